@@ -1,0 +1,574 @@
+/*
+ * oz2_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's Ozaki-scheme-II GEMM emulation
+ * (ptrkgtsch/mixed-GEMMul8, GEMMul8/src) used as the parity checker for the
+ * MI355X build.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product never links or calls it.
+ *
+ * Every stage follows the reference arithmetic operation by operation:
+ *   reductions ............ scaling.hpp:48-213  (thread-strided round-up sums
+ *                           and the wave64 __shfl_down tree, incl. the
+ *                           lane-1 partial-sum pickup at :190-195)
+ *   fast-mode shift ........ scaling.hpp:3373-3383
+ *   accurate-mode shift .... scaling.hpp:1504-1506, :1897-1941, :2215-2260,
+ *                           :2534-2559, :2679-2704, :3053-3136
+ *   residue encoding ....... scaling.hpp:215-230 (mod_8i), :693-751, :1091-1148
+ *   complex big matrix ..... scaling.hpp:753-838, :1150-1230
+ *   int8 GEMM + mod ........ gemmul8.cu:259-275, conv_32i_2_8u.hpp:7-71
+ *   CRT + epilogue ......... inverse_scaling.hpp:35-262, :268-1005
+ *   orchestration .......... gemmul8.cu:149-723
+ *
+ * Parity is pinned by tests/golden/ (vectors produced by the reference's own
+ * HIP build on MI355X, see tests/golden/README.md).  The one operation that is
+ * not reproduced bit-for-bit is __log2f (hardware v_log_f32 on gfx950); libm
+ * log2f stands in for it, which can move a shift by one in rare boundary
+ * cases -- the tests report the shift agreement rate separately.
+ *
+ * Build: oracle/Makefile (gcc -O3 -frounding-math -ffp-contract=off -fopenmp).
+ */
+#include <fenv.h>
+#include <limits.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../mixed-gemmul8_amd/csrc/oz2_tables.inc"
+
+#pragma STDC FENV_ACCESS ON
+
+/* ------------------------------------------------------------------ */
+/* directed-rounding primitives (OCML _ru/_rd equivalents)             */
+/* ------------------------------------------------------------------ */
+static double fma_ru(double a, double b, double c) {
+    fesetround(FE_UPWARD);
+    volatile double r = fma(a, b, c);
+    fesetround(FE_TONEAREST);
+    return r;
+}
+static float fmaf_ru(float a, float b, float c) {
+    fesetround(FE_UPWARD);
+    volatile float r = fmaf(a, b, c);
+    fesetround(FE_TONEAREST);
+    return r;
+}
+static float fmaf_rd(float a, float b, float c) {
+    fesetround(FE_DOWNWARD);
+    volatile float r = fmaf(a, b, c);
+    fesetround(FE_TONEAREST);
+    return r;
+}
+static double dadd_ru(double a, double b) {
+    fesetround(FE_UPWARD);
+    volatile double r = a + b;
+    fesetround(FE_TONEAREST);
+    return r;
+}
+static float fadd_ru(float a, float b) {
+    fesetround(FE_UPWARD);
+    volatile float r = a + b;
+    fesetround(FE_TONEAREST);
+    return r;
+}
+static float d2f_ru(double a) {
+    fesetround(FE_UPWARD);
+    volatile float r = (float)a;
+    fesetround(FE_TONEAREST);
+    return r;
+}
+/* v_cvt_i32_f32 semantics: saturating, NaN -> 0 */
+static int32_t cvt_i32(float x) {
+    if (isnan(x)) return 0;
+    if (x >= 2147483648.0f) return INT32_MAX;
+    if (x <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)x;
+}
+static int32_t f2i_rd(float x) { return cvt_i32(floorf(x)); }
+static int32_t d2i_ru(double x) {
+    double c = ceil(x);
+    if (isnan(c)) return 0;
+    if (c >= 2147483648.0) return INT32_MAX;
+    if (c <= -2147483648.0) return INT32_MIN;
+    return (int32_t)c;
+}
+static int32_t wrap32(int64_t v) { return (int32_t)(uint32_t)(uint64_t)v; }
+static int ilogb_d(double x) { return x == 0.0 ? INT32_MIN : ilogb(x); }
+static int ilogb_f(float x) { return x == 0.0f ? INT32_MIN : ilogbf(x); }
+static double scalbn_w(double x, int64_t e) { /* GPU wraps the int argument */
+    return scalbn(x, wrap32(e));
+}
+static float scalbnf_w(float x, int64_t e) { return scalbnf(x, wrap32(e)); }
+
+/* ------------------------------------------------------------------ */
+/* element access                                                      */
+/* ------------------------------------------------------------------ */
+/* type codes: 'd' f64, 's' f32, 'z' complex f64, 'c' complex f32 */
+static int is_cplx(char t) { return t == 'z' || t == 'c'; }
+static int is_dbl(char t) { return t == 'd' || t == 'z'; }
+
+/* element e of vector v of op(X): op N for A -> row v (stride ld), op T -> col v */
+typedef struct {
+    const void *base;
+    char t;
+    size_t ld;
+    int contiguous; /* 1: vector elements are adjacent (A op T / B op N) */
+} vec_src;
+
+static void load(const vec_src *s, size_t v, size_t e, double *re, double *im) {
+    size_t idx = s->contiguous ? v * s->ld + e : e * s->ld + v;
+    switch (s->t) {
+    case 'd': *re = ((const double *)s->base)[idx]; *im = 0; break;
+    case 's': *re = ((const float *)s->base)[idx]; *im = 0; break;
+    case 'z': *re = ((const double *)s->base)[2 * idx]; *im = ((const double *)s->base)[2 * idx + 1]; break;
+    default: *re = ((const float *)s->base)[2 * idx]; *im = ((const float *)s->base)[2 * idx + 1]; break;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* block reductions (scaling.hpp:48-213) on a gfx950 wave64 machine      */
+/* ------------------------------------------------------------------ */
+/* __shfl_down(width=64) tree over the 64 lanes of one wave, steps 16..1,
+ * out-of-range source lanes return the caller's own value (amd_warp_functions.h) */
+static void wave_tree_sum_d(double *v /*[64]*/) {
+    for (int d = 16; d >= 1; d >>= 1) {
+        double nv[64];
+        for (int l = 0; l < 64; ++l) nv[l] = dadd_ru(v[l], (l + d < 64) ? v[l + d] : v[l]);
+        memcpy(v, nv, sizeof(nv));
+    }
+}
+static void wave_tree_sum_f(float *v /*[64]*/) {
+    for (int d = 16; d >= 1; d >>= 1) {
+        float nv[64];
+        for (int l = 0; l < 64; ++l) nv[l] = fadd_ru(v[l], (l + d < 64) ? v[l + d] : v[l]);
+        memcpy(v, nv, sizeof(nv));
+    }
+}
+
+/* find_amax_and_nrm: VT threads (blockDim), thread t accumulates e = t, t+VT, ...
+ * Returns amax (exact max) and the reference's vecnrm: per 32-lane group the
+ * partial read at lane 1 (scaling.hpp:190-195), then the lane-32 tree over
+ * the group partials (:204-207). */
+static double amax_nrm_d(const vec_src *s, size_t v, size_t len, int VT, double *vecnrm) {
+    double part[512];
+    double amax = 0.0;
+    for (int t = 0; t < VT; ++t) {
+        double sum = 0.0;
+        for (size_t e = (size_t)t; e < len; e += (size_t)VT) {
+            double re, im;
+            load(s, v, e, &re, &im);
+            re = fabs(re);
+            if (is_cplx(s->t)) {
+                im = fabs(im);
+                double mx = re > im ? re : im;
+                if (mx > amax) amax = mx;
+                sum = fma_ru(re, re, sum);
+                sum = fma_ru(im, im, sum);
+            } else {
+                if (re > amax) amax = re;
+                sum = fma_ru(re, re, sum);
+            }
+        }
+        part[t] = sum;
+    }
+    double grp[32] = {0};
+    for (int w = 0; w < VT / 64; ++w) {
+        double lane[64];
+        memcpy(lane, part + 64 * w, sizeof(lane));
+        wave_tree_sum_d(lane);
+        grp[2 * w] = lane[1];
+        grp[2 * w + 1] = lane[33];
+    }
+    double lane[64] = {0};
+    for (int g = 0; g < VT / 32; ++g) lane[32 + g] = grp[g];
+    wave_tree_sum_d(lane);
+    *vecnrm = lane[32];
+    return amax;
+}
+static float amax_nrm_f(const vec_src *s, size_t v, size_t len, int VT, float *vecnrm) {
+    float part[512];
+    float amax = 0.0f;
+    for (int t = 0; t < VT; ++t) {
+        float sum = 0.0f;
+        for (size_t e = (size_t)t; e < len; e += (size_t)VT) {
+            double red, imd;
+            load(s, v, e, &red, &imd);
+            float re = fabsf((float)red), im = fabsf((float)imd);
+            if (is_cplx(s->t)) {
+                float mx = re > im ? re : im;
+                if (mx > amax) amax = mx;
+                sum = fmaf_ru(re, re, sum);
+                sum = fmaf_ru(im, im, sum);
+            } else {
+                if (re > amax) amax = re;
+                sum = fmaf_ru(re, re, sum);
+            }
+        }
+        part[t] = sum;
+    }
+    float grp[32] = {0};
+    for (int w = 0; w < VT / 64; ++w) {
+        float lane[64];
+        memcpy(lane, part + 64 * w, sizeof(lane));
+        wave_tree_sum_f(lane);
+        grp[2 * w] = lane[1];
+        grp[2 * w + 1] = lane[33];
+    }
+    float lane[64] = {0};
+    for (int g = 0; g < VT / 32; ++g) lane[32 + g] = grp[g];
+    wave_tree_sum_f(lane);
+    *vecnrm = lane[32];
+    return amax;
+}
+
+/* vecnorm::compute_sft (scaling.hpp:3373-3383) */
+static int32_t sft_fast_d(double amax, double vecnrm, float log2M) {
+    int e = ilogb_d(vecnrm);
+    double sc = scalbn_w(vecnrm, -(int64_t)e);
+    float vf = d2f_ru(sc);
+    float s = fadd_ru(log2f(vf), (float)e);
+    int32_t kk = f2i_rd(fmaf_rd(-0.51f, s, log2M));
+    int32_t lim = f2i_rd(log2M - 1.0f);
+    return wrap32((int64_t)(lim < kk ? lim : kk) - (int64_t)ilogb_d(amax));
+}
+static int32_t sft_fast_f(float amax, float vecnrm, float log2M) {
+    int32_t kk = f2i_rd(fmaf_rd(-0.51f, log2f(vecnrm), log2M));
+    int32_t lim = f2i_rd(log2M - 1.0f);
+    return wrap32((int64_t)(lim < kk ? lim : kk) - (int64_t)ilogb_f(amax));
+}
+/* int8tc::compute_sft (scaling.hpp:1504-1506) */
+static int32_t sft_accu(int32_t amax, int32_t sft0, float log2M) {
+    int32_t kk = f2i_rd(fmaf_rd(-0.51f, log2f((float)amax), log2M));
+    return wrap32((int64_t)sft0 + kk);
+}
+
+/* mod_8i (scaling.hpp:215-230): residue in [-p/2, p/2], then int8 wrap */
+static int8_t mod8_d(double a, unsigned j) {
+    double q = rint(a * oz2_rinv_d[j]);
+    float t = (float)fma(q, -(double)oz2_p[j], a);
+    float pf = -(float)oz2_p[j], rf = oz2_rinv_f[j];
+    t = fmaf(rintf(t * rf), pf, t);
+    t = fmaf(rintf(t * rf), pf, t);
+    return (int8_t)(uint8_t)(uint32_t)cvt_i32(t);
+}
+static int8_t mod8_f(float a, unsigned j) {
+    float pf = -(float)oz2_p[j], rf = oz2_rinv_f[j];
+    float t = fmaf(rintf(a * rf), pf, a);
+    t = fmaf(rintf(t * rf), pf, t);
+    t = fmaf(rintf(t * rf), pf, t);
+    t = fmaf(rintf(t * rf), pf, t);
+    return (int8_t)(uint8_t)(uint32_t)cvt_i32(t);
+}
+static int8_t neg8(int8_t x) { return (int8_t)(uint8_t)(-(int32_t)x); }
+
+/* trunc(scalbn(x, sft)) followed by N residues, into out[j*inc + pos] */
+static void encode(double x, int dbl, int32_t sft, unsigned N, int8_t *out, size_t inc, int negate) {
+    if (dbl) {
+        double y = trunc(scalbn_w(x, sft));
+        for (unsigned j = 0; j < N; ++j) {
+            int8_t r = mod8_d(y, j);
+            out[j * inc] = negate ? neg8(r) : r;
+        }
+    } else {
+        float y = truncf(scalbnf_w((float)x, sft));
+        for (unsigned j = 0; j < N; ++j) {
+            int8_t r = mod8_f(y, j);
+            out[j * inc] = negate ? neg8(r) : r;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* scaling stage                                                       */
+/* ------------------------------------------------------------------ */
+/* Slices: X8[j*(nv*kr) + v*kr + e], kr = k (real) or 2k (complex big
+ * matrix).  For complex A the big-matrix rows v and v+m are produced
+ * (scaling.hpp:753-838), for complex B the column [re; im] (:1150-1230). */
+static void fast_vectors(const vec_src *s, size_t nvec, size_t k, unsigned N, int VT, float log2M,
+                         int is_A, int8_t *X8, size_t nrows8, size_t kr, int16_t *sft_out) {
+    int dbl = is_dbl(s->t), cp = is_cplx(s->t);
+    size_t inc = nrows8 * kr;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (size_t v = 0; v < nvec; ++v) {
+        int32_t sft;
+        if (dbl) {
+            double nrm;
+            double amax = amax_nrm_d(s, v, k, VT, &nrm);
+            sft = sft_fast_d(amax, nrm, log2M);
+        } else {
+            float nrm;
+            float amax = amax_nrm_f(s, v, k, VT, &nrm);
+            sft = sft_fast_f(amax, nrm, log2M);
+        }
+        sft_out[v] = (int16_t)(uint16_t)(uint32_t)wrap32(-(int64_t)sft);
+        for (size_t e = 0; e < k; ++e) {
+            double re, im;
+            load(s, v, e, &re, &im);
+            if (!cp) {
+                encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
+            } else if (is_A) {
+                encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
+                encode(im, dbl, sft, N, X8 + v * kr + k + e, inc, 1);
+                encode(im, dbl, sft, N, X8 + (v + nvec) * kr + e, inc, 0);
+                encode(re, dbl, sft, N, X8 + (v + nvec) * kr + k + e, inc, 0);
+            } else {
+                encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
+                encode(im, dbl, sft, N, X8 + v * kr + k + e, inc, 0);
+            }
+        }
+    }
+}
+
+/* 6-bit magnitude extraction (extract_A8i_kernel / extract_B8i_kernel) */
+static void extract6(const vec_src *s, size_t nvec, size_t k, int8_t *X6, int16_t *sft0) {
+    int dbl = is_dbl(s->t);
+#pragma omp parallel for schedule(static)
+    for (size_t v = 0; v < nvec; ++v) {
+        double amax = 0.0;
+        for (size_t e = 0; e < k; ++e) {
+            double re, im;
+            load(s, v, e, &re, &im);
+            double a = dbl ? fabs(re) : (double)fabsf((float)re);
+            if (a > amax) amax = a;
+        }
+        int32_t sf = dbl ? wrap32(5 - (int64_t)ilogb_d(amax)) : wrap32(5 - (int64_t)ilogb_f((float)amax));
+        sft0[v] = (int16_t)sf;
+        for (size_t e = 0; e < k; ++e) {
+            double re, im;
+            load(s, v, e, &re, &im);
+            int32_t q = dbl ? d2i_ru(scalbn_w(fabs(re), sf)) : d2i_ru((double)scalbnf_w(fabsf((float)re), sf));
+            X6[v * k + e] = (int8_t)(uint8_t)(uint32_t)q;
+        }
+    }
+}
+
+static void accurate_vectors(const vec_src *s, size_t nvec, size_t k, unsigned N, const int32_t *amax_bound,
+                             const int16_t *sft0, float log2M, int8_t *X8, size_t kr, int16_t *sft_out) {
+    int dbl = is_dbl(s->t);
+    size_t inc = nvec * kr;
+#pragma omp parallel for schedule(dynamic, 4)
+    for (size_t v = 0; v < nvec; ++v) {
+        int32_t sft = sft_accu(amax_bound[v], sft0[v], log2M);
+        sft_out[v] = (int16_t)(uint16_t)(uint32_t)wrap32(-(int64_t)sft);
+        for (size_t e = 0; e < k; ++e) {
+            double re, im;
+            load(s, v, e, &re, &im);
+            encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* public entry points                                                 */
+/* ------------------------------------------------------------------ */
+/* opA/opB: 0 = N, 1 = T.  VT: threads_scaling of the reference entry point
+ * (gemmul8.cu:206-222 etc.: 128 for gemm<double>, mixed and complex, 512 for
+ * gemm<float>).  Returns 0 on success. */
+int oz2o_scaling(char ta, char tb, int opA, int opB, size_t m, size_t n, size_t k, const void *A, size_t lda,
+                 const void *B, size_t ldb, unsigned N, int fastmode, int VT, int8_t *A8, int8_t *B8,
+                 int16_t *sftA, int16_t *sftB) {
+    if (N < 2 || N > 20) return -1;
+    int cp = is_cplx(ta) || is_cplx(tb);
+    if (cp && (!is_cplx(ta) || !is_cplx(tb))) return -2;
+    if (cp && (opA != 0 || opB != 0)) return -3;
+    vec_src sa = {A, ta, lda, opA != 0};
+    vec_src sb = {B, tb, ldb, opB == 0};
+    size_t kr = cp ? 2 * k : k;
+    size_t mr = cp ? 2 * m : m;
+    if (fastmode) {
+        float log2M = oz2_log2M_fast[N - 2];
+        fast_vectors(&sa, m, k, N, VT, log2M, 1, A8, mr, kr, sftA);
+        fast_vectors(&sb, n, k, N, VT, log2M, 0, B8, n, kr, sftB);
+        return 0;
+    }
+    if (cp) return -4; /* complex accurate mode: not restated */
+    int8_t *A6 = (int8_t *)malloc(m * k), *B6 = (int8_t *)malloc(n * k);
+    int16_t *s0A = (int16_t *)malloc(m * 2), *s0B = (int16_t *)malloc(n * 2);
+    int32_t *amA = (int32_t *)calloc(m, 4), *amB = (int32_t *)calloc(n, 4);
+    extract6(&sa, m, k, A6, s0A);
+    extract6(&sb, n, k, B6, s0B);
+    /* bound product C32 = A6 * B6^T, then row / column max of |C32| */
+#pragma omp parallel for schedule(static)
+    for (size_t r = 0; r < m; ++r) {
+        int32_t mx = 0;
+        for (size_t c = 0; c < n; ++c) {
+            int32_t acc = 0;
+            for (size_t e = 0; e < k; ++e) acc += (int32_t)A6[r * k + e] * (int32_t)B6[c * k + e];
+            int32_t a = acc < 0 ? -acc : acc;
+            if (a > mx) mx = a;
+        }
+        amA[r] = mx;
+    }
+#pragma omp parallel for schedule(static)
+    for (size_t c = 0; c < n; ++c) {
+        int32_t mx = 0;
+        for (size_t r = 0; r < m; ++r) {
+            int32_t acc = 0;
+            for (size_t e = 0; e < k; ++e) acc += (int32_t)A6[r * k + e] * (int32_t)B6[c * k + e];
+            int32_t a = acc < 0 ? -acc : acc;
+            if (a > mx) mx = a;
+        }
+        amB[c] = mx;
+    }
+    float log2M = oz2_log2M_accu[N - 2];
+    accurate_vectors(&sa, m, k, N, amA, s0A, log2M, A8, kr, sftA);
+    accurate_vectors(&sb, n, k, N, amB, s0B, log2M, B8, kr, sftB);
+    free(A6); free(B6); free(s0A); free(s0B); free(amA); free(amB);
+    return 0;
+}
+
+/* conv_32i_2_8u (conv_32i_2_8u.hpp:7-56) */
+static uint8_t conv8(int32_t x, unsigned j) {
+    if (j == 0) return (uint8_t)(uint32_t)x;
+    int32_t p = oz2_p[j];
+    int32_t q = (int32_t)(((int64_t)x * (int64_t)oz2_barrett[j]) >> 32); /* __mulhi */
+    x -= q * p;
+    x -= (x >= p) * p;
+    x += (x < 0) * p;
+    return (uint8_t)x;
+}
+
+/* residues R[j*(mr*n) + c*mr + r] = (A8[j] row r . B8[j] col c) mod p_j */
+int oz2o_residues(size_t mr, size_t n, size_t kr, unsigned N, const int8_t *A8, const int8_t *B8, uint8_t *R) {
+    for (unsigned j = 0; j < N; ++j) {
+        const int8_t *a = A8 + (size_t)j * mr * kr;
+        const int8_t *b = B8 + (size_t)j * n * kr;
+        uint8_t *o = R + (size_t)j * mr * n;
+#pragma omp parallel for schedule(static)
+        for (size_t c = 0; c < n; ++c) {
+            for (size_t r = 0; r < mr; ++r) {
+                int32_t acc = 0;
+                const int8_t *ar = a + r * kr, *bc = b + c * kr;
+                for (size_t e = 0; e < kr; ++e) acc += (int32_t)ar[e] * (int32_t)bc[e];
+                o[c * mr + r] = conv8(acc, j);
+            }
+        }
+    }
+    return 0;
+}
+
+/* CRT value of one residue column position (inverse_scaling.hpp:35-62, 138-172) */
+static double crt_value(const uint8_t *R, size_t plane, size_t idx, unsigned N, int numM1) {
+    const unsigned t = N - 2;
+    if (numM1) {
+        double C = 0.0;
+        for (unsigned i = 0; i < N; ++i) C = fma(oz2_NMi_1[t][i], (double)R[i * plane + idx], C);
+        double quot = -rint(C * oz2_invM[t]);
+        return fma(quot, oz2_M_hi[t], C);
+    }
+    double C1 = 0.0, C2 = 0.0;
+    for (unsigned i = 0; i < N; ++i) {
+        double r = (double)R[i * plane + idx];
+        C1 = fma(oz2_NMi_2[N - 8][i][0], r, C1);
+        C2 = fma(oz2_NMi_2[N - 8][i][1], r, C2);
+    }
+    double quot = -rint(fma(C1, oz2_invM[t], C2 * oz2_invM[t]));
+    double t1 = fma(quot, oz2_M_hi[t], C1) + C2;
+    return fma(quot, oz2_M_lo[t], t1);
+}
+
+/* BLAS-correct epilogue selection used by the MI355X build; with quirks=1
+ * the reference's variants are restated verbatim (inverse_scaling.hpp:417
+ * beta*AB + C, :736/:763 alpha*C + AB). */
+static double epi_d(double v, double c, double al, double be, int numM1, int quirks) {
+    if (al == 1.0) {
+        if (be == 0.0) return v;
+        if (be == 1.0) return c + v;
+        return quirks ? fma(be, v, c) : fma(be, c, v);
+    }
+    if (be == 1.0) return (quirks && !numM1) ? fma(al, c, v) : fma(al, v, c);
+    return fma(be, c, al * v);
+}
+static float epi_f(float v, float c, float al, float be, int quirks) {
+    if (al == 1.0f) {
+        if (be == 0.0f) return v;
+        if (be == 1.0f) return c + v;
+        return quirks ? fmaf(be, v, c) : fmaf(be, c, v);
+    }
+    if (be == 1.0f) return fmaf(al, v, c);
+    return fmaf(be, c, al * v);
+}
+
+/* tc: output type; m, n: logical C size; R planes of size mr*n (mr = m or 2m) */
+int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint8_t *R, const int16_t *sftA,
+             const int16_t *sftB, const void *alpha, const void *beta, void *C, size_t ldc, int quirks) {
+    if (N < 2 || N > 20) return -1;
+    int numM1 = (oz2_numM[N - 2] == 1) || tc == 's' || tc == 'c';
+    size_t mr = complex_bm ? 2 * m : m;
+    size_t plane = mr * n;
+#pragma omp parallel for schedule(static)
+    for (size_t c = 0; c < n; ++c) {
+        for (size_t r = 0; r < m; ++r) {
+            int sft = (int)sftA[r] + (int)sftB[c];
+            double vr = scalbn(crt_value(R, plane, c * mr + r, N, numM1), sft);
+            size_t o = c * ldc + r;
+            if (!complex_bm) {
+                if (tc == 'd') {
+                    double *Cd = (double *)C;
+                    Cd[o] = epi_d(vr, Cd[o], *(const double *)alpha, *(const double *)beta, numM1, quirks);
+                } else {
+                    float *Cf = (float *)C;
+                    Cf[o] = epi_f((float)vr, Cf[o], *(const float *)alpha, *(const float *)beta, quirks);
+                }
+            } else {
+                double vi = scalbn(crt_value(R, plane, c * mr + r + m, N, numM1), sft);
+                if (tc == 'z') {
+                    const double *al = (const double *)alpha, *be = (const double *)beta;
+                    double *Cz = (double *)C;
+                    double cr = Cz[2 * o], ci = Cz[2 * o + 1];
+                    if (al[0] == 1.0 && al[1] == 0.0 && be[0] == 0.0 && be[1] == 0.0) {
+                        Cz[2 * o] = vr; Cz[2 * o + 1] = vi;
+                    } else { /* alpha*v + beta*c, products fused as the GPU build does */
+                        double tr = fma(al[0], vr, -al[1] * vi), ti = fma(al[0], vi, al[1] * vr);
+                        Cz[2 * o] = fma(be[0], cr, fma(-be[1], ci, tr));
+                        Cz[2 * o + 1] = fma(be[0], ci, fma(be[1], cr, ti));
+                    }
+                } else {
+                    const float *al = (const float *)alpha, *be = (const float *)beta;
+                    float *Cc = (float *)C;
+                    float fr = (float)vr, fi = (float)vi;
+                    float cr = Cc[2 * o], ci = Cc[2 * o + 1];
+                    if (al[0] == 1.0f && al[1] == 0.0f && be[0] == 0.0f && be[1] == 0.0f) {
+                        Cc[2 * o] = fr; Cc[2 * o + 1] = fi;
+                    } else {
+                        float tr = fmaf(al[0], fr, -al[1] * fi), ti = fmaf(al[0], fi, al[1] * fr);
+                        Cc[2 * o] = fmaf(be[0], cr, fmaf(-be[1], ci, tr));
+                        Cc[2 * o + 1] = fmaf(be[0], ci, fmaf(be[1], cr, ti));
+                    }
+                }
+            }
+        }
+    }
+    return 0;
+}
+
+/* Whole gemm: C = alpha*op(A)*op(B) + beta*C.  Optional outputs sftA/sftB
+ * (may be NULL).  complex_bm selects COMPLEX_BIG_MATRIX_ENCODE. */
+int oz2o_gemm(char ta, char tb, char tc, int opA, int opB, size_t m, size_t n, size_t k, const void *alpha,
+              const void *A, size_t lda, const void *B, size_t ldb, const void *beta, void *C, size_t ldc,
+              unsigned N, int fastmode, int VT, int quirks, int16_t *sftA_out, int16_t *sftB_out) {
+    int cp = is_cplx(ta);
+    size_t kr = cp ? 2 * k : k, mr = cp ? 2 * m : m;
+    int8_t *A8 = (int8_t *)malloc((size_t)N * mr * kr + 1);
+    int8_t *B8 = (int8_t *)malloc((size_t)N * n * kr + 1);
+    uint8_t *R = (uint8_t *)malloc((size_t)N * mr * n + 1);
+    int16_t *sA = (int16_t *)malloc(m * 2 + 2), *sB = (int16_t *)malloc(n * 2 + 2);
+    int rc = oz2o_scaling(ta, tb, opA, opB, m, n, k, A, lda, B, ldb, N, fastmode, VT, A8, B8, sA, sB);
+    if (rc == 0) rc = oz2o_residues(mr, n, kr, N, A8, B8, R);
+    if (rc == 0) rc = oz2o_crt(tc, cp, m, n, N, R, sA, sB, alpha, beta, C, ldc, quirks);
+    if (sftA_out) memcpy(sftA_out, sA, m * 2);
+    if (sftB_out) memcpy(sftB_out, sB, n * 2);
+    free(A8); free(B8); free(R); free(sA); free(sB);
+    return rc;
+}
+
+int oz2o_num_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
+}
