@@ -1,0 +1,78 @@
+/* gemmul8_c.h -- C ABI of the MI355X-native Ozaki-scheme-II GEMM emulator.
+ *
+ * Plain pointers and sizes only (no C++ / torch types), for ctypes, cgo, JNI or
+ * any FFI.  The reference has no C ABI; each entry below replaces one C++ entry
+ * point of GEMMul8/include/gemmul8.hpp:
+ *
+ *   gemmul8_work_size  <- gemmul8::workSize            (gemmul8.hpp:18-22, gemmul8.cu:129-147)
+ *   gemmul8_gemm       <- gemmul8::gemm<TA,TB,TC>      (gemmul8.hpp:29-287, gemmul8.cu:149-1316)
+ *                         stream instead of hipblasHandle_t, dtype codes instead of template args
+ *
+ * All device pointers are column-major HIP device memory; alpha/beta are host
+ * pointers to one TC value; the work buffer is caller-owned (>= work size).
+ * Return codes: 0 ok, GEMMUL8_E_* < 0 on invalid arguments (nothing enqueued).
+ */
+#ifndef GEMMUL8_C_H
+#define GEMMUL8_C_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { GEMMUL8_OP_N = 0, GEMMUL8_OP_T = 1, GEMMUL8_OP_C = 2 };
+enum { GEMMUL8_R_64F = 0, GEMMUL8_R_32F = 1, GEMMUL8_C_64F = 2, GEMMUL8_C_32F = 3 };
+enum { GEMMUL8_REAL_DEFAULT = 0, GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE = 1, GEMMUL8_COMPLEX_CLASSIC_MULT = 2,
+       GEMMUL8_COMPLEX_KARATSUBA_MULT = 3 };
+enum {
+    GEMMUL8_OK = 0,
+    GEMMUL8_E_MODULI = -1,       /* num_moduli outside [2, 20] */
+    GEMMUL8_E_TYPES = -2,        /* unsupported dtype combination for compute_type */
+    GEMMUL8_E_OP = -3,           /* unsupported transpose op */
+    GEMMUL8_E_SIZE = -4,         /* k beyond the int32-exact bound (2^17), or a leading dimension too small */
+    GEMMUL8_E_UNSUPPORTED = -5,  /* compute type / mode not implemented on this build */
+    GEMMUL8_E_HIP = -6           /* a HIP launch or runtime call failed */
+};
+
+/* bytes of workspace required by gemmul8_gemm for this shape (0 for an unknown compute_type) */
+size_t gemmul8_work_size(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type);
+
+/* C = alpha * op(A) * op(B) + beta * C, emulated with num_moduli int8 products.
+ * stream: hipStream_t (NULL = null stream).  fastmode: 1 = vecnorm shifts, 0 = accurate (int8 bound product).
+ * phase_ns: optional double[4]; when non-NULL the call waits for its own completion and stores the
+ * phase times {scaling, int8 products, conversion (fused: 0), inverse scaling} in nanoseconds. */
+int gemmul8_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b, int type_c,
+                 const void *alpha, const void *A, size_t lda, const void *B, size_t ldb, const void *beta, void *C,
+                 size_t ldc, unsigned num_moduli, int fastmode, void *work, int compute_type, double *phase_ns);
+
+/* --- instrumentation (used by bench.py / tests) --------------------------------------------- */
+/* When enabled, every gemmul8_gemm records HIP events between its phases on its stream; the
+ * accumulated per-phase milliseconds and the call count are read (and reset) with
+ * gemmul8_timing_read, which synchronises on the recorded events. */
+void gemmul8_timing_enable(int on);
+int gemmul8_timing_read(double *phase_ms /* [4] */, int *calls);
+
+/* Workspace layout for a shape: fills out[0..15] = {m_pad, n_pad, k_pad, ksteps, planeA, planeB,
+ * planeR, offA, offB, offR, offSftA, offSftB, offBound, offSft0, total, kblk}. */
+int gemmul8_layout(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, size_t *out);
+
+/* Validation hook: int32 product of plane 0 of the tiled int8 operands already in `work`
+ * (layout of gemmul8_layout) into C32 (column-major, ld = m_pad).  Used by the MFMA tests. */
+int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type,
+                           void *work, int32_t *C32);
+
+/* --- bench / test harness (not part of the emulation path) ------------------------------------ */
+/* The reference's input generator (testing/make_matrix.hpp:8-71): x = (U(0,1] - 0.5) * exp(phi * N(0,1))
+ * from hiprand XORWOW, init(seed, idx, 0); complex draws (u_re, n_re, u_im, n_im). dtype: GEMMUL8_*. */
+int gemmul8_randmat(void *stream, int dtype, size_t m, size_t n, void *A, double phi, unsigned long long seed);
+/* Double-double reference product C1 + C2 = A * B (testing/eval.hpp:265-308); A m x k, B k x n, col-major. */
+int gemmul8_dd_gemm(void *stream, size_t m, size_t n, size_t k, const double *A, const double *B, double *C1,
+                    double *C2);
+/* err[i] = |C[i] - (C1[i] + C2[i])| / |C1[i] + C2[i]| evaluated in double-double (eval.hpp:317-338). */
+int gemmul8_relerr_dd(void *stream, size_t count, const double *C, const double *C1, const double *C2, double *err);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GEMMUL8_C_H */

@@ -1,0 +1,326 @@
+// gemmul8.hip -- orchestration, the drop-in C++ API (include/gemmul8.hpp) and the C ABI
+// (include/gemmul8_c.h) of the MI355X Ozaki-scheme-II emulator.
+//
+// Per call, on ONE stream and with no device-wide synchronisation:
+//   fast mode      stats(A), stats(B) -> encode(A), encode(B)            split.hip
+//   accurate mode  amax(A,B) -> 6-bit magnitudes -> bound product -> shifts -> encode
+//   products       one launch, all moduli, fused mod-p epilogue         gemm_i8.hip
+//   recombination  CRT + scaling + alpha/beta                           crt.hip
+// The reference runs the same phases with 4N+4 hipDeviceSynchronize calls, a
+// per-modulus hipblasGemmEx and a separate conversion kernel (gemmul8.cu:149-723).
+#include <cstdio>
+#include <mutex>
+#include <vector>
+
+#include "../../include/gemmul8.hpp"
+#include "../../include/gemmul8_c.h"
+#include "oz2_split.hpp"
+
+namespace oz2 {
+
+struct Call {
+    OperandDesc A, B;
+    size_t m, n, k;
+    unsigned N;
+    bool fast;
+    bool cplx;
+    OutType ot;
+    const void *alpha, *beta;
+    void *C;
+    size_t ldc;
+    void *work;
+    int VT;
+    hipStream_t st;
+};
+
+// ---------------- phase timing (HIP events on the call's stream) ----------------
+namespace timing {
+static std::mutex mu;
+static bool enabled = false;
+struct Rec {
+    hipEvent_t ev[4];  // after split, after products, (conversion = products), after crt
+    hipEvent_t start;
+};
+static std::vector<Rec> pending;
+static std::vector<Rec> pool;
+static double acc_ms[4] = {0, 0, 0, 0};
+static int calls = 0;
+
+static Rec acquire() {
+    Rec r;
+    if (!pool.empty()) {
+        r = pool.back();
+        pool.pop_back();
+        return r;
+    }
+    (void)hipEventCreate(&r.start);
+    for (auto &e : r.ev) (void)hipEventCreate(&e);
+    return r;
+}
+static void resolve_all() {
+    for (auto &r : pending) {
+        (void)hipEventSynchronize(r.ev[3]);
+        float a = 0, b = 0, c = 0;
+        (void)hipEventElapsedTime(&a, r.start, r.ev[0]);
+        (void)hipEventElapsedTime(&b, r.ev[0], r.ev[1]);
+        (void)hipEventElapsedTime(&c, r.ev[2], r.ev[3]);
+        acc_ms[0] += a;
+        acc_ms[1] += b;
+        acc_ms[3] += c;
+        ++calls;
+        pool.push_back(r);
+    }
+    pending.clear();
+}
+}  // namespace timing
+
+static inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
+
+static int run(const Call &c, double *phase_ns) {
+    const Layout L = make_layout(c.m, c.n, c.k, c.N, c.cplx);
+    int8_t *base = static_cast<int8_t *>(c.work);
+    int8_t *A8 = base + L.offA;
+    int8_t *B8 = base + L.offB;
+    uint8_t *R = reinterpret_cast<uint8_t *>(base + L.offR);
+    int16_t *sftA = reinterpret_cast<int16_t *>(base + L.offSftA);
+    int16_t *sftB = reinterpret_cast<int16_t *>(base + L.offSftB);
+    int32_t *bound = reinterpret_cast<int32_t *>(base + L.offBound);
+    int16_t *sft0 = reinterpret_cast<int16_t *>(base + L.offSft0);
+    const ModParams MP = make_mod_params(c.N);
+    const CrtParams CP = make_crt_params(c.N, c.ot == OutType::F32 || c.ot == OutType::C32);
+
+    const bool want_events = phase_ns != nullptr;
+    bool record;
+    timing::Rec rec{};
+    {
+        std::lock_guard<std::mutex> g(timing::mu);
+        record = want_events || timing::enabled;
+        if (record) rec = timing::acquire();
+    }
+    if (record) (void)hipEventRecord(rec.start, c.st);
+
+    if (c.fast) {
+        const float log2M = oz2_log2M_fast[c.N - 2];
+        split_stats(c.A, c.k, c.m, c.VT, false, log2M, sftA, c.st);
+        split_stats(c.B, c.k, c.n, c.VT, false, log2M, sftB, c.st);
+    } else {
+        const float log2M = oz2_log2M_accu[c.N - 2];
+        split_stats(c.A, c.k, c.m, c.VT, true, 0.f, sft0, c.st);
+        split_stats(c.B, c.k, c.n, c.VT, true, 0.f, sft0 + L.m_pad, c.st);
+        split_encode(c.A, true, c.m, c.k, sft0, A8, L.planeA, L, 1, MP, c.st);
+        split_encode(c.B, false, c.n, c.k, sft0 + L.m_pad, B8, L.planeB, L, 1, MP, c.st);
+        (void)hipMemsetAsync(bound, 0, (L.m_pad + L.n_pad) * sizeof(int32_t), c.st);
+        gemm_i8(A8, B8, L, 1, Epi::BOUND, nullptr, bound, bound + L.m_pad, MP, c.st);
+        split_finalize_accurate(sft0, bound, c.m, log2M, sftA, c.st);
+        split_finalize_accurate(sft0 + L.m_pad, bound + L.m_pad, c.n, log2M, sftB, c.st);
+    }
+    split_encode(c.A, true, c.m, c.k, sftA, A8, L.planeA, L, 0, MP, c.st);
+    split_encode(c.B, false, c.n, c.k, sftB, B8, L.planeB, L, 0, MP, c.st);
+    if (record) (void)hipEventRecord(rec.ev[0], c.st);
+
+    gemm_i8(A8, B8, L, c.N, Epi::RESIDUE, R, nullptr, nullptr, MP, c.st);
+    if (record) {
+        (void)hipEventRecord(rec.ev[1], c.st);
+        (void)hipEventRecord(rec.ev[2], c.st);
+    }
+
+    crt_inverse(R, L, sftA, sftB, CP, c.ot, c.alpha, c.beta, c.C, c.ldc, c.st);
+    if (record) (void)hipEventRecord(rec.ev[3], c.st);
+    if (!launch_ok()) return GEMMUL8_E_HIP;
+
+    if (want_events) {
+        (void)hipEventSynchronize(rec.ev[3]);
+        float a = 0, b = 0, d = 0;
+        (void)hipEventElapsedTime(&a, rec.start, rec.ev[0]);
+        (void)hipEventElapsedTime(&b, rec.ev[0], rec.ev[1]);
+        (void)hipEventElapsedTime(&d, rec.ev[2], rec.ev[3]);
+        phase_ns[0] = a * 1e6;
+        phase_ns[1] = b * 1e6;
+        phase_ns[2] = 0.0;
+        phase_ns[3] = d * 1e6;
+    }
+    if (record) {
+        std::lock_guard<std::mutex> g(timing::mu);
+        if (timing::enabled) timing::pending.push_back(rec);
+        else timing::pool.push_back(rec);
+    }
+    return GEMMUL8_OK;
+}
+
+// dtype helpers
+static bool dt_dbl(int t) { return t == GEMMUL8_R_64F || t == GEMMUL8_C_64F; }
+static bool dt_cplx(int t) { return t == GEMMUL8_C_64F || t == GEMMUL8_C_32F; }
+
+static int prepare(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int ta, int tb, int tc,
+                   const void *alpha, const void *A, size_t lda, const void *B, size_t ldb, const void *beta, void *C,
+                   size_t ldc, unsigned N, int fast, void *work, int ctype, Call &c) {
+    if (N < 2 || N > 20) return GEMMUL8_E_MODULI;
+    if (ta < 0 || ta > 3 || tb < 0 || tb > 3 || tc < 0 || tc > 3) return GEMMUL8_E_TYPES;
+    const bool cp = dt_cplx(ta);
+    if (dt_cplx(tb) != cp || dt_cplx(tc) != cp) return GEMMUL8_E_TYPES;
+    if (cp && ctype != GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE) {
+        if (ctype == GEMMUL8_COMPLEX_CLASSIC_MULT || ctype == GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_UNSUPPORTED;
+        return GEMMUL8_E_TYPES;
+    }
+    if (!cp && ctype != GEMMUL8_REAL_DEFAULT) return GEMMUL8_E_TYPES;
+    // output precision is the higher of the inputs' in every reference specialization (gemmul8.hpp:49-287)
+    if (!cp && !(tc == GEMMUL8_R_64F || tc == GEMMUL8_R_32F)) return GEMMUL8_E_TYPES;
+    if (op_a < 0 || op_a > 2 || op_b < 0 || op_b > 2) return GEMMUL8_E_OP;
+    if (cp && (op_a != GEMMUL8_OP_N || op_b != GEMMUL8_OP_N)) return GEMMUL8_E_UNSUPPORTED;
+    if (cp && !fast) return GEMMUL8_E_UNSUPPORTED;
+    const size_t kr = cp ? 2 * round_up(k, KSTEP) : round_up(k, KSTEP);
+    if (kr > ((size_t)1 << 17)) return GEMMUL8_E_SIZE;
+    const bool ta_t = op_a != GEMMUL8_OP_N, tb_t = op_b != GEMMUL8_OP_N;
+    if (lda < (ta_t ? k : m) || ldb < (tb_t ? n : k) || ldc < m) return GEMMUL8_E_SIZE;
+    c.A = OperandDesc{A, lda, ta_t, dt_dbl(ta), cp};
+    c.B = OperandDesc{B, ldb, !tb_t, dt_dbl(tb), cp};
+    c.m = m; c.n = n; c.k = k; c.N = N;
+    c.fast = fast != 0;
+    c.cplx = cp;
+    c.ot = static_cast<OutType>(tc);
+    c.alpha = alpha; c.beta = beta; c.C = C; c.ldc = ldc; c.work = work;
+    // threads_scaling of the matching reference entry point (gemmul8.cu:218-222, 361-365, 502-506, 648-652):
+    // 512 for gemm<float>, 128 for gemm<double>, the mixed and the complex paths
+    c.VT = (ta == GEMMUL8_R_32F && tb == GEMMUL8_R_32F && tc == GEMMUL8_R_32F) ? 512 : 128;
+    c.st = static_cast<hipStream_t>(stream);
+    return GEMMUL8_OK;
+}
+
+}  // namespace oz2
+
+// =============================== C ABI ===================================
+extern "C" {
+
+size_t gemmul8_work_size(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type) {
+    if (compute_type < 0 || compute_type > 3) return 0;
+    const bool cp = compute_type != GEMMUL8_REAL_DEFAULT;
+    return oz2::make_layout(m, n, k, num_moduli, cp).total;
+}
+
+int gemmul8_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b, int type_c,
+                 const void *alpha, const void *A, size_t lda, const void *B, size_t ldb, const void *beta, void *C,
+                 size_t ldc, unsigned num_moduli, int fastmode, void *work, int compute_type, double *phase_ns) {
+    oz2::Call c{};
+    const int rc = oz2::prepare(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, alpha, A, lda, B, ldb, beta, C,
+                                ldc, num_moduli, fastmode, work, compute_type, c);
+    if (rc != GEMMUL8_OK) return rc;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    return oz2::run(c, phase_ns);
+}
+
+void gemmul8_timing_enable(int on) {
+    std::lock_guard<std::mutex> g(oz2::timing::mu);
+    oz2::timing::enabled = on != 0;
+}
+
+int gemmul8_timing_read(double *phase_ms, int *calls) {
+    std::lock_guard<std::mutex> g(oz2::timing::mu);
+    oz2::timing::resolve_all();
+    for (int i = 0; i < 4; ++i) {
+        phase_ms[i] = oz2::timing::acc_ms[i];
+        oz2::timing::acc_ms[i] = 0;
+    }
+    *calls = oz2::timing::calls;
+    oz2::timing::calls = 0;
+    return GEMMUL8_OK;
+}
+
+int gemmul8_layout(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, size_t *out) {
+    const oz2::Layout L = oz2::make_layout(m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
+    const size_t v[16] = {L.m_pad, L.n_pad, L.k_pad, L.ksteps, L.planeA, L.planeB, L.planeR, L.offA,
+                          L.offB, L.offR, L.offSftA, L.offSftB, L.offBound, L.offSft0, L.total, L.kblk};
+    for (int i = 0; i < 16; ++i) out[i] = v[i];
+    return GEMMUL8_OK;
+}
+
+int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type,
+                           void *work, int32_t *C32) {
+    const oz2::Layout L = oz2::make_layout(m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
+    int8_t *base = static_cast<int8_t *>(work);
+    const oz2::ModParams MP = oz2::make_mod_params(num_moduli);
+    oz2::gemm_i8(base + L.offA, base + L.offB, L, 1, oz2::Epi::RAW, C32, nullptr, nullptr, MP,
+                 static_cast<hipStream_t>(stream));
+    return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+}  // extern "C"
+
+// =========================== drop-in C++ API ===============================
+namespace gemmul8 {
+
+// the reference's own per-encoding size functions are exported symbols (gemmul8.cu:27-127)
+size_t workSize_real(const size_t m, const size_t n, const size_t k, const unsigned num_moduli) {
+    return oz2::make_layout(m, n, k, num_moduli, false).total;
+}
+size_t workSize_bigmatrix(const size_t m, const size_t n, const size_t k, const unsigned num_moduli) {
+    return oz2::make_layout(m, n, k, num_moduli, true).total;
+}
+size_t workSize_kara(const size_t m, const size_t n, const size_t k, const unsigned num_moduli) {
+    return oz2::make_layout(m, n, k, num_moduli, true).total;
+}
+
+size_t workSize(const size_t m, const size_t n, const size_t k, const unsigned num_moduli,
+                const computeType_t computeType) {
+    switch (computeType) {
+    case REAL_DEFAULT: return workSize_real(m, n, k, num_moduli);
+    case COMPLEX_BIG_MATRIX_ENCODE: return workSize_bigmatrix(m, n, k, num_moduli);
+    case COMPLEX_CLASSIC_MULT:
+    case COMPLEX_KARATSUBA_MULT: return workSize_kara(m, n, k, num_moduli);
+    default: fprintf(stderr, "Unknown compute type\n"); return 0;
+    }
+}
+
+template <typename T> struct dtype_of;
+template <> struct dtype_of<double> { static constexpr int v = GEMMUL8_R_64F; };
+template <> struct dtype_of<float> { static constexpr int v = GEMMUL8_R_32F; };
+template <> struct dtype_of<hipDoubleComplex> { static constexpr int v = GEMMUL8_C_64F; };
+template <> struct dtype_of<hipFloatComplex> { static constexpr int v = GEMMUL8_C_32F; };
+
+static int op_code(hipblasOperation_t op) {
+    return op == HIPBLAS_OP_N ? GEMMUL8_OP_N : (op == HIPBLAS_OP_T ? GEMMUL8_OP_T : GEMMUL8_OP_C);
+}
+
+template <typename TA, typename TB, typename TC>
+static std::vector<double> gemm_impl(hipblasHandle_t handle, hipblasOperation_t op_A, hipblasOperation_t op_B,
+                                     size_t m, size_t n, size_t k, const TC *alpha, const TA *A, size_t lda,
+                                     const TB *B, size_t ldb, const TC *beta, TC *C, size_t ldc, unsigned num_moduli,
+                                     bool fastmode, void *work, computeType_t computeType) {
+    std::vector<double> timer(4, 0.0);
+    hipStream_t st = nullptr;
+    if (handle) (void)hipblasGetStream(handle, &st);
+    const int rc = gemmul8_gemm(st, op_code(op_A), op_code(op_B), m, n, k, dtype_of<TA>::v, dtype_of<TB>::v,
+                                dtype_of<TC>::v, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fastmode ? 1 : 0,
+                                work, (int)computeType, timer.data());
+    if (rc == GEMMUL8_E_TYPES) fprintf(stderr, "Unsupported compute type for the argument types.\n");
+    else if (rc != GEMMUL8_OK) fprintf(stderr, "gemmul8::gemm: invalid arguments or unsupported mode (code %d)\n", rc);
+    if (rc != GEMMUL8_OK) return std::vector<double>(4, 0.0);
+    return timer;
+}
+
+#define GEMMUL8_DEFINE(TA_, TB_, TC_)                                                                              \
+    template <>                                                                                                    \
+    std::vector<double> gemm<TA_, TB_, TC_>(hipblasHandle_t handle, const hipblasOperation_t op_A,                  \
+                                            const hipblasOperation_t op_B, const size_t m, const size_t n,          \
+                                            const size_t k, const TC_ *alpha, const TA_ *const A, const size_t lda, \
+                                            const TB_ *const B, const size_t ldb, const TC_ *beta, TC_ *const C,    \
+                                            const size_t ldc, const unsigned num_moduli, const bool fastmode,      \
+                                            void *const work, const computeType_t computeType) {                  \
+        return gemm_impl<TA_, TB_, TC_>(handle, op_A, op_B, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc,          \
+                                        num_moduli, fastmode, work, computeType);                                  \
+    }
+
+GEMMUL8_DEFINE(double, double, double)
+GEMMUL8_DEFINE(float, float, float)
+GEMMUL8_DEFINE(double, float, double)
+GEMMUL8_DEFINE(float, double, double)
+GEMMUL8_DEFINE(double, float, float)
+GEMMUL8_DEFINE(float, double, float)
+GEMMUL8_DEFINE(hipFloatComplex, hipFloatComplex, hipFloatComplex)
+GEMMUL8_DEFINE(hipDoubleComplex, hipDoubleComplex, hipDoubleComplex)
+GEMMUL8_DEFINE(hipFloatComplex, hipDoubleComplex, hipDoubleComplex)
+GEMMUL8_DEFINE(hipDoubleComplex, hipFloatComplex, hipDoubleComplex)
+GEMMUL8_DEFINE(hipDoubleComplex, hipFloatComplex, hipFloatComplex)
+GEMMUL8_DEFINE(hipFloatComplex, hipDoubleComplex, hipFloatComplex)
+#undef GEMMUL8_DEFINE
+
+}  // namespace gemmul8

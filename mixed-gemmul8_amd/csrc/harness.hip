@@ -1,0 +1,165 @@
+// harness.hip -- bench/test utilities exported through the C ABI (not on the emulation path).
+//
+//  * gemmul8_randmat: the reference test drivers' input generator
+//    (GEMMul8/testing/make_matrix.hpp:8-71): hiprand XORWOW, init(seed, idx, 0),
+//    x = (u - 0.5) * exp(phi * n); same library, same stream of draws.
+//  * gemmul8_dd_gemm: double-double reference product (testing/eval.hpp:265-308),
+//    TwoProd + double-double accumulation, LDS-tiled.
+//  * gemmul8_relerr_dd: |C - Cref| / |Cref| in double-double (eval.hpp:317-338).
+#include <hip/hip_runtime.h>
+#include <hiprand/hiprand_kernel.h>
+
+#include "../../include/gemmul8_c.h"
+
+namespace oz2h {
+
+template <typename T>
+__global__ void randmat_kernel(size_t total, T *A, double phi, unsigned long long seed) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    hiprandState_t state;
+    hiprand_init(seed, idx, 0, &state);
+    const T u = static_cast<T>(hiprand_uniform_double(&state));
+    const T nn = static_cast<T>(hiprand_normal_double(&state));
+    A[idx] = static_cast<T>((u - 0.5) * exp(nn * static_cast<T>(phi)));
+}
+
+template <typename T>
+__global__ void randmat_c_kernel(size_t total, T *A, double phi, unsigned long long seed) {
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    hiprandState_t state;
+    hiprand_init(seed, idx, 0, &state);
+    const T ur = static_cast<T>(hiprand_uniform_double(&state));
+    const T nr = static_cast<T>(hiprand_normal_double(&state));
+    const T ui = static_cast<T>(hiprand_uniform_double(&state));
+    const T ni = static_cast<T>(hiprand_normal_double(&state));
+    A[2 * idx] = static_cast<T>((ur - 0.5) * exp(nr * static_cast<T>(phi)));
+    A[2 * idx + 1] = static_cast<T>((ui - 0.5) * exp(ni * static_cast<T>(phi)));
+}
+
+// ---- double-double helpers (eval.hpp:22-110 semantics) ----
+__device__ __forceinline__ void two_sum(double a, double b, double &c, double &d) {
+    c = a + b;
+    const double s = c - a, t = b - s, u = c - s;
+    d = (a - u) + t;
+}
+__device__ __forceinline__ void fast_two_sum(double a, double b, double &c, double &d) {
+    c = a + b;
+    d = (a - c) + b;
+}
+__device__ __forceinline__ void dd_add(double a1, double a2, double b1, double b2, double &c1, double &c2) {
+    two_sum(a1, b1, c1, c2);
+    c2 += a2;
+    c2 += b2;
+    fast_two_sum(c1, c2, c1, c2);
+}
+
+// C1 + C2 = A * B, 64x64 output tile per 256-thread block, 4x4 outputs per thread
+__global__ __launch_bounds__(256) void dd_gemm_kernel(size_t m, size_t n, size_t k, const double *__restrict__ A,
+                                                      const double *__restrict__ B, double *C1, double *C2) {
+    __shared__ double As[16][65];
+    __shared__ double Bs[16][65];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const size_t r0 = (size_t)blockIdx.x * 64, c0 = (size_t)blockIdx.y * 64;
+    double s1[4][4] = {}, s2[4][4] = {};
+    for (size_t kk = 0; kk < k; kk += 16) {
+        for (int i = threadIdx.x; i < 16 * 64; i += 256) {
+            const int rr = i & 63, kq = i >> 6;
+            const size_t r = r0 + rr, kx = kk + kq;
+            As[kq][rr] = (r < m && kx < k) ? A[kx * m + r] : 0.0;
+            const int cc = i >> 4, kq2 = i & 15;
+            const size_t c = c0 + cc, ky = kk + kq2;
+            Bs[kq2][cc] = (c < n && ky < k) ? B[c * k + ky] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int q = 0; q < 16; ++q) {
+            double a[4], b[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) a[i] = As[q][ty + 16 * i];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = Bs[q][tx + 16 * j];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const double p1 = a[i] * b[j];
+                    const double p2 = __builtin_fma(a[i], b[j], -p1);
+                    dd_add(p1, p2, s1[i][j], s2[i][j], s1[i][j], s2[i][j]);
+                }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const size_t r = r0 + ty + 16 * i, c = c0 + tx + 16 * j;
+            if (r < m && c < n) {
+                C1[c * m + r] = s1[i][j];
+                C2[c * m + r] = s2[i][j];
+            }
+        }
+}
+
+__global__ void relerr_kernel(size_t count, const double *C, const double *C1, const double *C2, double *err) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    // dd::sub(C, 0, C1, C2) then dd::div(., C1, C2) (eval.hpp:65-110, 317-338)
+    double d1, d2;
+    {
+        const double a1 = C[i], b1 = C1[i], b2 = C2[i];
+        d1 = a1 - b1;
+        const double s = d1 - a1, t = b1 + s, u = d1 - s;
+        d2 = (a1 - u) - t;
+        d2 -= b2;
+        fast_two_sum(d1, d2, d1, d2);
+    }
+    const double b1 = C1[i], b2 = C2[i];
+    double q1 = d1 / b1;
+    const double s = q1 * b1, t = __builtin_fma(q1, b1, -s);
+    double u = d1 - s;
+    u -= t;
+    u += d2;
+    u = __builtin_fma(-q1, b2, u);
+    u /= b1;
+    double q2;
+    fast_two_sum(q1, u, q1, q2);
+    err[i] = fabs(q1);
+}
+
+}  // namespace oz2h
+
+extern "C" {
+
+int gemmul8_randmat(void *stream, int dtype, size_t m, size_t n, void *A, double phi, unsigned long long seed) {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const size_t total = m * n;
+    if (total == 0) return GEMMUL8_OK;
+    const unsigned grid = (unsigned)((total + 255) / 256);
+    switch (dtype) {
+    case GEMMUL8_R_64F: oz2h::randmat_kernel<double><<<grid, 256, 0, st>>>(total, (double *)A, phi, seed); break;
+    case GEMMUL8_R_32F: oz2h::randmat_kernel<float><<<grid, 256, 0, st>>>(total, (float *)A, phi, seed); break;
+    case GEMMUL8_C_64F: oz2h::randmat_c_kernel<double><<<grid, 256, 0, st>>>(total, (double *)A, phi, seed); break;
+    case GEMMUL8_C_32F: oz2h::randmat_c_kernel<float><<<grid, 256, 0, st>>>(total, (float *)A, phi, seed); break;
+    default: return GEMMUL8_E_TYPES;
+    }
+    return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_dd_gemm(void *stream, size_t m, size_t n, size_t k, const double *A, const double *B, double *C1,
+                    double *C2) {
+    dim3 grid((unsigned)((m + 63) / 64), (unsigned)((n + 63) / 64));
+    oz2h::dd_gemm_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(m, n, k, A, B, C1, C2);
+    return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_relerr_dd(void *stream, size_t count, const double *C, const double *C1, const double *C2, double *err) {
+    if (count == 0) return GEMMUL8_OK;
+    oz2h::relerr_kernel<<<(unsigned)((count + 255) / 256), 256, 0, static_cast<hipStream_t>(stream)>>>(count, C, C1,
+                                                                                                       C2, err);
+    return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+}  // extern "C"

@@ -1,0 +1,160 @@
+// oz2_common.hpp -- shared definitions of the MI355X (gfx950) Ozaki-II GEMM emulator.
+//
+// Data layout in HBM (one workspace, caller-owned, see oz2_layout below):
+//
+//   slice planes   int8  [N][vtile][kstep][16 KiB]   for A (rows of op(A)) and B (cols of op(B))
+//                  A 16 KiB panel holds 256 vectors x 64 k-bytes, pre-arranged in MFMA
+//                  fragment order: [s:2][blk:8][h:2][r:32][16 B] with
+//                  vector = 32*blk + r, k = 32*s + 16*h + byte.  A wave's operand read of
+//                  one 32x32 fragment is therefore one contiguous 1 KiB ds_read_b128 sweep,
+//                  and the panel is staged HBM->LDS by linear global_load_lds (no swizzle
+//                  math, no bank conflicts, no power-of-two row strides in HBM).
+//   residue planes uint8 [N][n_pad][m_pad]          column-major, value in [0, p_i)
+//   sftA, sftB     int16                            exponents (reference convention: -shift)
+//   bound          int32 [m_pad + n_pad]            accurate mode: row/col max |A6 B6^T|
+//   sft0           int16 [m_pad + n_pad]            accurate mode: 5 - ilogb(amax)
+//
+// The reference keeps K-contiguous slices with ld = k rounded to 16 (+64 when a
+// multiple of 1024) and a separate int32 product buffer (GEMMul8/src/gemmul8.cu:182-234);
+// the tiled layout above replaces both.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef OCML_BASIC_ROUNDED_OPERATIONS
+#error "build with -DOCML_BASIC_ROUNDED_OPERATIONS (directed-rounding intrinsics)"
+#endif
+
+#include "oz2_tables.inc"
+
+namespace oz2 {
+
+constexpr int TILE = 256;          // vectors per panel (GEMM block tile edge)
+constexpr int KSTEP = 64;          // k-bytes per panel
+constexpr int PANEL = TILE * KSTEP;  // 16 KiB
+
+enum class Scal : int { F64 = 0, F32 = 1 };
+
+struct Layout {
+    // logical problem
+    size_t m, n, k;  // complex: logical complex sizes
+    unsigned N;
+    bool cplx;
+    // int8 product shape
+    size_t mr, kr;       // rows of the int8 A (m or 2m), k-extent incl. complex blocks
+    size_t kblk;         // k padded to KSTEP (offset of the imaginary block for complex)
+    size_t m_pad, n_pad, k_pad;
+    size_t ksteps, mtiles, ntiles;
+    size_t planeA, planeB, planeR;  // bytes per modulus
+    // workspace offsets (bytes)
+    size_t offA, offB, offR, offSftA, offSftB, offBound, offSft0, total;
+};
+
+static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool cplx) {
+    Layout L{};
+    L.m = m; L.n = n; L.k = k; L.N = N; L.cplx = cplx;
+    L.kblk = round_up(k, KSTEP);
+    L.mr = cplx ? 2 * m : m;
+    L.kr = cplx ? 2 * L.kblk : L.kblk;
+    L.m_pad = round_up(L.mr, TILE);
+    L.n_pad = round_up(n, TILE);
+    L.k_pad = L.kr;
+    L.ksteps = L.k_pad / KSTEP;
+    L.mtiles = L.m_pad / TILE;
+    L.ntiles = L.n_pad / TILE;
+    L.planeA = L.m_pad * L.k_pad;
+    L.planeB = L.n_pad * L.k_pad;
+    L.planeR = L.m_pad * L.n_pad;
+    size_t off = 0;
+    L.offA = off; off += round_up(L.planeA * N, 256);
+    L.offB = off; off += round_up(L.planeB * N, 256);
+    L.offR = off; off += round_up(L.planeR * N, 256);
+    L.offSftA = off; off += round_up(L.m_pad * 2, 256);
+    L.offSftB = off; off += round_up(L.n_pad * 2, 256);
+    L.offBound = off; off += round_up((L.m_pad + L.n_pad) * 4, 256);
+    L.offSft0 = off; off += round_up((L.m_pad + L.n_pad) * 2, 256);
+    L.total = off;
+    return L;
+}
+
+// byte offset of the 16-B chunk holding (vector v, k-bytes kk..kk+15), kk % 16 == 0
+__host__ __device__ inline size_t panel_offset(size_t v, size_t kk, size_t ksteps) {
+    return ((v >> 8) * ksteps + (kk >> 6)) * (size_t)PANEL + ((kk >> 5) & 1) * 8192 + ((v >> 5) & 7) * 1024 +
+           (((kk >> 4) & 1) * 32 + (v & 31)) * 16;
+}
+
+// ------------------------------------------------------------------
+// CRT constants passed by value (kernarg), replacing the reference's
+// per-call hipMemcpyToSymbol into __constant__ (gemmul8.cu:236-241)
+// ------------------------------------------------------------------
+struct CrtParams {
+    double w_hi[OZ2_MAX_MODULI];  // NMi_2 hi (numM = 2) or NMi_1 (numM = 1)
+    double w_lo[OZ2_MAX_MODULI];  // NMi_2 lo
+    double invM, M1, M2;
+    int numM1;
+    unsigned N;
+};
+
+struct ModParams {
+    int p[OZ2_MAX_MODULI];
+    int barrett[OZ2_MAX_MODULI];
+    double rinv_d[OZ2_MAX_MODULI];
+    float rinv_f[OZ2_MAX_MODULI];
+    unsigned N;
+};
+
+static inline ModParams make_mod_params(unsigned N) {
+    ModParams P{};
+    for (int i = 0; i < OZ2_MAX_MODULI; ++i) {
+        P.p[i] = oz2_p[i];
+        P.barrett[i] = oz2_barrett[i];
+        P.rinv_d[i] = oz2_rinv_d[i];
+        P.rinv_f[i] = oz2_rinv_f[i];
+    }
+    P.N = N;
+    return P;
+}
+
+static inline CrtParams make_crt_params(unsigned N, bool force_numM1) {
+    CrtParams C{};
+    const unsigned t = N - 2;
+    C.numM1 = (oz2_numM[t] == 1) || force_numM1;
+    C.N = N;
+    for (unsigned i = 0; i < N; ++i) {
+        if (C.numM1) {
+            C.w_hi[i] = oz2_NMi_1[t][i];
+        } else {
+            C.w_hi[i] = oz2_NMi_2[N - 8][i][0];
+            C.w_lo[i] = oz2_NMi_2[N - 8][i][1];
+        }
+    }
+    C.invM = oz2_invM[t];
+    C.M1 = oz2_M_hi[t];
+    C.M2 = oz2_M_lo[t];
+    return C;
+}
+
+// ------------------------------------------------------------------
+// device arithmetic shared by the split kernels
+// ------------------------------------------------------------------
+// residue of an integer-valued x in [-p/2, p/2] as int8 (v_cvt_i32_f32 + byte pack,
+// i.e. +128 wraps to -128), restating mod_8i (scaling.hpp:215-230)
+__device__ __forceinline__ int mod8_f64(double x, int p, double rinv, float rinvf) {
+    float t = __double2float_rn(__builtin_fma(__builtin_rint(x * rinv), -(double)p, x));
+    const float pf = -(float)p;
+    t = __builtin_fmaf(__builtin_rintf(t * rinvf), pf, t);
+    t = __builtin_fmaf(__builtin_rintf(t * rinvf), pf, t);
+    return (int)t;
+}
+__device__ __forceinline__ int mod8_f32(float x, int p, float rinvf) {
+    const float pf = -(float)p;
+    float t = __builtin_fmaf(__builtin_rintf(x * rinvf), pf, x);
+    t = __builtin_fmaf(__builtin_rintf(t * rinvf), pf, t);
+    t = __builtin_fmaf(__builtin_rintf(t * rinvf), pf, t);
+    t = __builtin_fmaf(__builtin_rintf(t * rinvf), pf, t);
+    return (int)t;
+}
+
+}  // namespace oz2

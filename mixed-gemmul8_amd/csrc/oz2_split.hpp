@@ -1,0 +1,41 @@
+// oz2_split.hpp -- internal launcher interface of the gfx950 kernels.
+#pragma once
+#include "oz2_common.hpp"
+
+namespace oz2 {
+
+// One operand as the kernels see it: vector v = row of op(A) or column of op(B),
+// element e runs along k.  contig: element e of vector v is at ptr[v*ld + e]
+// (B op N, A op T); otherwise at ptr[e*ld + v] (A op N, B op T).
+struct OperandDesc {
+    const void *ptr;
+    size_t ld;     // leading dimension in elements (complex: in complex elements)
+    bool contig;
+    bool dbl;      // real part is f64 (else f32)
+    bool cplx;
+};
+
+// ---- split.hip ----
+// VT = threads_scaling of the reference entry point (128 or 512); accurate=true
+// writes sft0 = 5 - ilogb(amax) instead of the fast-mode shift.
+void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool accurate, float log2M, int16_t *out,
+                 hipStream_t st);
+// mode 0: N residue planes from sft (reference convention -shift); mode 1: 6-bit magnitudes from sft0
+void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
+                  size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st);
+void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
+                             hipStream_t st);
+
+// ---- gemm_i8.hip ----
+enum class Epi : int { RESIDUE = 0, BOUND = 1, RAW = 2 };
+// Products of the N slice planes: residue planes (uint8, [N][n_pad][m_pad]),
+// bound (rowmax[m_pad], colmax[n_pad] of |C|, must be zeroed), or raw int32 (plane 0 only).
+void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
+             int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st);
+
+// ---- crt.hip ----
+enum class OutType : int { F64 = 0, F32 = 1, C64 = 2, C32 = 3 };
+void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const int16_t *sftB, const CrtParams &CP,
+                 OutType ot, const void *alpha, const void *beta, void *C, size_t ldc, hipStream_t st);
+
+}  // namespace oz2

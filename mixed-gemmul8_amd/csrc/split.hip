@@ -1,0 +1,384 @@
+// split.hip -- slice extraction and residue encoding for gfx950 ("scaling" stage).
+//
+// Two passes per operand, both HBM-streaming:
+//   1. stats:  per vector (row of op(A) / column of op(B)) amax and the round-up
+//              sum of squares, reduced in exactly the order the reference reduces
+//              them on gfx950 (thread-strided partials of `VT` threads, wave64
+//              __shfl_down tree, lane-1 group pickup -- GEMMul8/src/scaling.hpp:155-213),
+//              then the shift (vecnorm::compute_sft, scaling.hpp:3373-3383).  The
+//              partials are computed from coalesced loads: a strided (column-major
+//              row) vector is swept 16 rows at a time, so every wave load is a
+//              contiguous run of rows instead of the reference's lda-strided walk
+//              or its stair_kernel copy (scaling.hpp:232-239, 3703-3710).
+//   2. encode: 64-vector x 64-element tiles staged through LDS, trunc(x*2^sft),
+//              N residues per element (mod_8i, scaling.hpp:215-230), written as
+//              16-byte chunks straight into the MFMA-ready panel layout.
+// Accurate mode adds the 6-bit magnitude extraction (scaling.hpp:1897-1941,
+// 2215-2260) whose bound product runs on the int8 GEMM kernel (gemm_i8.hip).
+#include "oz2_split.hpp"
+
+namespace oz2 {
+
+template <typename R> __device__ __forceinline__ R fma_ru(R a, R b, R c);
+template <> __device__ __forceinline__ double fma_ru<double>(double a, double b, double c) { return __fma_ru(a, b, c); }
+template <> __device__ __forceinline__ float fma_ru<float>(float a, float b, float c) { return __fmaf_ru(a, b, c); }
+template <typename R> __device__ __forceinline__ R add_ru(R a, R b);
+template <> __device__ __forceinline__ double add_ru<double>(double a, double b) { return __dadd_ru(a, b); }
+template <> __device__ __forceinline__ float add_ru<float>(float a, float b) { return __fadd_ru(a, b); }
+
+// reference wave tree: __shfl_down width 64, steps 16..1 (inner_warp_sum on wave64)
+template <typename R> __device__ __forceinline__ R ref_wave_sum(R v) {
+#pragma unroll
+    for (int d = 16; d >= 1; d >>= 1) v = add_ru<R>(v, __shfl_down(v, d));
+    return v;
+}
+template <typename R> __device__ __forceinline__ R wave_max(R v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = fmax(v, __shfl_xor(v, d));
+    return v;
+}
+
+// vecnorm::compute_sft (scaling.hpp:3373-3383)
+__device__ __forceinline__ int compute_sft(double amax, double vecnrm, float log2M) {
+    const int e = ilogb(vecnrm);
+    const float vf = __double2float_ru(scalbn(vecnrm, -e));
+    const int kk = __float2int_rd(__fmaf_rd(-0.51F, __fadd_ru(__log2f(vf), (float)e), log2M));
+    return min(__float2int_rd(log2M - 1.0f), kk) - ilogb(amax);
+}
+__device__ __forceinline__ int compute_sft(float amax, float vecnrm, float log2M) {
+    const int kk = __float2int_rd(__fmaf_rd(-0.51F, __log2f(vecnrm), log2M));
+    return min(__float2int_rd(log2M - 1.0f), kk) - ilogbf(amax);
+}
+
+template <typename R, bool CPLX>
+__device__ __forceinline__ void load_elem(const R *__restrict__ X, size_t idx, R &re, R &im) {
+    if constexpr (CPLX) {
+        using V2 = typename std::conditional<std::is_same<R, double>::value, double2, float2>::type;
+        V2 z = reinterpret_cast<const V2 *>(X)[idx];
+        re = z.x;
+        im = z.y;
+    } else {
+        re = X[idx];
+        im = 0;
+    }
+}
+
+template <typename R, bool CPLX>
+__device__ __forceinline__ void accum(R re, R im, R &amax, R &sum) {
+    re = fabs(re);
+    if constexpr (CPLX) {
+        im = fabs(im);
+        amax = fmax(amax, fmax(re, im));
+        sum = fma_ru<R>(re, re, sum);
+        sum = fma_ru<R>(im, im, sum);
+    } else {
+        amax = fmax(amax, re);
+        sum = fma_ru<R>(re, re, sum);
+    }
+}
+
+// ------------------------------------------------------------------
+// pass 1a: contiguous vectors (B op N, A op T): one vector per VT-thread block
+// ------------------------------------------------------------------
+template <typename R, bool CPLX, int VT, bool ACCU>
+__global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
+                                                         float log2M, int16_t *__restrict__ sft_out) {
+    const size_t v = blockIdx.x;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const R *__restrict__ x = X + (CPLX ? 2 : 1) * v * ld;
+    R amax = 0, sum = 0;
+    for (size_t e = t; e < len; e += VT) {
+        R re, im;
+        load_elem<R, CPLX>(x, e, re, im);
+        accum<R, CPLX>(re, im, amax, sum);
+    }
+    __shared__ R grp[32];
+    __shared__ R gmax[8];
+    amax = wave_max<R>(amax);
+    if (!ACCU) {
+        sum = ref_wave_sum<R>(sum);
+        if (lane == 1) grp[2 * w] = sum;
+        if (lane == 33) grp[2 * w + 1] = sum;
+    }
+    if (lane == 0) gmax[w] = amax;
+    __syncthreads();
+    if (w == 0) {
+        R mx = lane < VT / 64 ? gmax[lane] : R(0);
+        mx = wave_max<R>(mx);
+        if (ACCU) {
+            if (lane == 0) sft_out[v] = (int16_t)(5 - (std::is_same<R, double>::value ? ilogb((double)mx) : ilogbf((float)mx)));
+        } else {
+            R s2 = (lane >= 32 && lane - 32 < VT / 32) ? grp[lane - 32] : R(0);
+            s2 = ref_wave_sum<R>(s2);
+            const R nrm = __shfl(s2, 32);
+            if (lane == 0) sft_out[v] = (int16_t)(-compute_sft(mx, nrm, log2M));
+        }
+    }
+}
+
+// ------------------------------------------------------------------
+// pass 1b: strided vectors (A op N, B op T): 16 vectors per 256-thread block,
+// coalesced 16-row sweeps; virtual thread t of the reference = slot + 16*c
+// ------------------------------------------------------------------
+template <typename R, bool CPLX, int VT, bool ACCU>
+__global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
+                                                           float log2M, int16_t *__restrict__ sft_out) {
+    constexpr int NA = VT / 16;
+    const int tid = threadIdx.x, row = tid & 15, slot = tid >> 4;
+    const size_t v = (size_t)blockIdx.x * 16 + row;
+    R acc[NA];
+#pragma unroll
+    for (int c = 0; c < NA; ++c) acc[c] = 0;
+    R amax = 0;
+    if (v < nvec) {
+        for (size_t b = 0; b < len; b += VT) {
+#pragma unroll
+            for (int c = 0; c < NA; ++c) {
+                const size_t e = b + slot + 16 * c;
+                if (e < len) {
+                    R re, im;
+                    load_elem<R, CPLX>(X, e * ld + v, re, im);
+                    accum<R, CPLX>(re, im, amax, acc[c]);
+                }
+            }
+        }
+    }
+    __shared__ R part[16][VT + 1];
+    __shared__ R pmax[16][17];
+    if (!ACCU) {
+#pragma unroll
+        for (int c = 0; c < NA; ++c) part[row][slot + 16 * c] = acc[c];
+    }
+    pmax[row][slot] = amax;
+    __syncthreads();
+    const int w = tid >> 6, lane = tid & 63;
+#pragma unroll 1
+    for (int rr = 0; rr < 4; ++rr) {
+        const int r2 = w * 4 + rr;
+        const size_t v2 = (size_t)blockIdx.x * 16 + r2;
+        R mx = lane < 16 ? pmax[r2][lane] : R(0);
+        mx = wave_max<R>(mx);
+        if (ACCU) {
+            if (lane == 0 && v2 < nvec)
+                sft_out[v2] = (int16_t)(5 - (std::is_same<R, double>::value ? ilogb((double)mx) : ilogbf((float)mx)));
+            continue;
+        }
+        R gv = 0;
+#pragma unroll
+        for (int vw = 0; vw < VT / 64; ++vw) {
+            R s = ref_wave_sum<R>(part[r2][64 * vw + lane]);
+            const R g0 = __shfl(s, 1), g1 = __shfl(s, 33);
+            if (lane == 32 + 2 * vw) gv = g0;
+            if (lane == 33 + 2 * vw) gv = g1;
+        }
+        gv = ref_wave_sum<R>(gv);
+        const R nrm = __shfl(gv, 32);
+        if (lane == 0 && v2 < nvec) sft_out[v2] = (int16_t)(-compute_sft(mx, nrm, log2M));
+    }
+}
+
+// ------------------------------------------------------------------
+// pass 2: encode.  Tile = 64 vectors x KT elements through LDS.
+//   MODE 0: residues of trunc(x * 2^sft), N planes (fast & accurate modes)
+//   MODE 1: 6-bit magnitudes ceil(|x| * 2^sft0), 1 plane (accurate-mode bound)
+// Complex A (IS_A): row v <- [re, -im], row v+m <- [im, re]  (scaling.hpp:753-838)
+// Complex B:        col v <- [re; im]                           (scaling.hpp:1150-1230)
+// ------------------------------------------------------------------
+template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
+__global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__restrict__ X, size_t ld, size_t nvec,
+                                                                   size_t len, const int16_t *__restrict__ sft,
+                                                                   int8_t *__restrict__ out, size_t plane,
+                                                                   size_t ksteps, size_t kblk, size_t vmax,
+                                                                   ModParams MP) {
+    constexpr int KT = CPLX ? 32 : 64;
+    constexpr int NT = CPLX ? 128 : 256;
+    constexpr int NC = CPLX ? 2 : 1;
+    const size_t v0 = (size_t)blockIdx.x * 64, e0 = (size_t)blockIdx.y * KT;
+    const int tid = threadIdx.x;
+    __shared__ R tile[KT][64 + 1][NC];
+
+    // stage the tile, coalesced along whichever index is contiguous in HBM
+#pragma unroll
+    for (int i = 0; i < (64 * KT) / NT; ++i) {
+        const int idx = tid + NT * i;
+        int vl, el;
+        if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
+        const size_t v = v0 + vl, e = e0 + el;
+        R re = 0, im = 0;
+        if (v < nvec && e < len) load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, re, im);
+        tile[el][vl][0] = re;
+        if (CPLX) tile[el][vl][NC - 1] = im;
+    }
+    __syncthreads();
+
+    const int vl = tid & 63, c = tid >> 6;  // c-th 16-element chunk of the tile
+    const size_t v = v0 + vl;
+    const size_t kk = e0 + 16 * c;
+    int s = 0;
+    if (v < nvec) s = MODE == 0 ? -(int)sft[v] : (int)sft[v];
+
+    R yr[16], yi[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        R re = tile[16 * c + q][vl][0];
+        R im = CPLX ? tile[16 * c + q][vl][NC - 1] : R(0);
+        if (MODE == 0) {
+            yr[q] = trunc(scalbn(re, s));
+            yi[q] = trunc(scalbn(im, s));
+        } else {
+            yr[q] = scalbn(fabs(re), s);
+        }
+    }
+
+    if (MODE == 1) {
+        uint32_t w[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int q = 4 * d + b;
+                const int val = std::is_same<R, double>::value ? __double2int_ru((double)yr[q]) : __float2int_ru((float)yr[q]);
+                acc |= ((uint32_t)val & 0xffu) << (8 * b);
+            }
+            w[d] = acc;
+        }
+        *reinterpret_cast<uint4 *>(out + panel_offset(v, kk, ksteps)) = make_uint4(w[0], w[1], w[2], w[3]);
+        return;
+    }
+
+    const bool top = v < nvec || !CPLX || !IS_A;  // complex A: rows >= m only emit their (zero) bottom copy
+    for (unsigned j = 0; j < MP.N; ++j) {
+        const int p = MP.p[j];
+        const double rd = MP.rinv_d[j];
+        const float rf = MP.rinv_f[j];
+        uint32_t wr[4], wi[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            uint32_t ar = 0, ai = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int q = 4 * d + b;
+                int rr, ri = 0;
+                if constexpr (std::is_same<R, double>::value) {
+                    rr = mod8_f64(yr[q], p, rd, rf);
+                    if (CPLX) ri = mod8_f64(yi[q], p, rd, rf);
+                } else {
+                    rr = mod8_f32(yr[q], p, rf);
+                    if (CPLX) ri = mod8_f32(yi[q], p, rf);
+                }
+                ar |= ((uint32_t)rr & 0xffu) << (8 * b);
+                ai |= ((uint32_t)ri & 0xffu) << (8 * b);
+            }
+            wr[d] = ar;
+            wi[d] = ai;
+        }
+        int8_t *o = out + (size_t)j * plane;
+        if (!CPLX) {
+            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+        } else if (IS_A) {
+            // -im as bytes: per-byte two's complement negation
+            uint32_t ni[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                uint32_t r = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) r |= ((0u - ((wi[d] >> (8 * b)) & 0xffu)) & 0xffu) << (8 * b);
+                ni[d] = r;
+            }
+            const size_t vb = v + nvec;  // bottom row (v + m)
+            if (top) {
+                *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+                *reinterpret_cast<uint4 *>(o + panel_offset(v, kblk + kk, ksteps)) = make_uint4(ni[0], ni[1], ni[2], ni[3]);
+            }
+            if (vb < vmax) {
+                *reinterpret_cast<uint4 *>(o + panel_offset(vb, kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
+                *reinterpret_cast<uint4 *>(o + panel_offset(vb, kblk + kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+            }
+        } else {
+            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+            *reinterpret_cast<uint4 *>(o + panel_offset(v, kblk + kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
+        }
+    }
+}
+
+// accurate mode: sft = sft0 + floor_rd(-0.51*log2(amax) + log2M)  (int8tc::compute_sft, scaling.hpp:1504-1506)
+__global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, const int32_t *__restrict__ bound,
+                                             size_t nvec, float log2M, int16_t *__restrict__ sft_out) {
+    const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= nvec) return;
+    const int amax = bound[v];
+    const int s = (int)sft0[v] + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
+    sft_out[v] = (int16_t)(-s);
+}
+
+// ------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------
+template <typename R, bool CPLX>
+static void launch_stats(const void *X, size_t ld, bool contig, size_t len, size_t nvec, int VT, bool accurate,
+                         float log2M, int16_t *out, hipStream_t st) {
+    const R *x = static_cast<const R *>(X);
+    if (contig) {
+#define OZ2_SC(vt, ac) stats_contig_kernel<R, CPLX, vt, ac><<<dim3((unsigned)nvec), dim3(vt), 0, st>>>(x, ld, len, nvec, log2M, out)
+        if (VT == 512) { if (accurate) OZ2_SC(512, true); else OZ2_SC(512, false); }
+        else { if (accurate) OZ2_SC(128, true); else OZ2_SC(128, false); }
+#undef OZ2_SC
+    } else {
+        const unsigned g = (unsigned)((nvec + 15) / 16);
+#define OZ2_SS(vt, ac) stats_strided_kernel<R, CPLX, vt, ac><<<dim3(g), dim3(256), 0, st>>>(x, ld, len, nvec, log2M, out)
+        if (VT == 512) { if (accurate) OZ2_SS(512, true); else OZ2_SS(512, false); }
+        else { if (accurate) OZ2_SS(128, true); else OZ2_SS(128, false); }
+#undef OZ2_SS
+    }
+}
+
+template <typename R, bool CPLX, bool IS_A>
+static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, size_t len, const int16_t *sft,
+                          int8_t *out, size_t plane, const Layout &L, size_t vpad_grid, size_t vmax, int mode,
+                          const ModParams &MP, hipStream_t st) {
+    constexpr int KT = CPLX ? 32 : 64;
+    constexpr int NT = CPLX ? 128 : 256;
+    const R *x = static_cast<const R *>(X);
+    dim3 grid((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
+#define OZ2_EN(cg, md) encode_kernel<R, CPLX, cg, IS_A, md><<<grid, dim3(NT), 0, st>>>(x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, MP)
+    if (contig) { if (mode == 0) OZ2_EN(true, 0); else OZ2_EN(true, 1); }
+    else { if (mode == 0) OZ2_EN(false, 0); else OZ2_EN(false, 1); }
+#undef OZ2_EN
+}
+
+void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool accurate, float log2M, int16_t *out,
+                 hipStream_t st) {
+    if (d.dbl) {
+        if (d.cplx) launch_stats<double, true>(d.ptr, d.ld, d.contig, len, nvec, VT, accurate, log2M, out, st);
+        else launch_stats<double, false>(d.ptr, d.ld, d.contig, len, nvec, VT, accurate, log2M, out, st);
+    } else {
+        if (d.cplx) launch_stats<float, true>(d.ptr, d.ld, d.contig, len, nvec, VT, accurate, log2M, out, st);
+        else launch_stats<float, false>(d.ptr, d.ld, d.contig, len, nvec, VT, accurate, log2M, out, st);
+    }
+}
+
+void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
+                  size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st) {
+    // grid extent over vectors: padded rows/cols get zero slices; complex A covers
+    // [0, m_pad - m) so that rows [2m, m_pad) are zeroed through their bottom copy
+    size_t vpad = is_A ? (d.cplx ? L.m_pad - L.m : L.m_pad) : L.n_pad;
+    vpad = round_up(vpad, 64);
+    const size_t vmax = is_A ? L.m_pad : L.n_pad;
+#define OZ2_LE(R, C, A) launch_encode<R, C, A>(d.ptr, d.ld, d.contig, nvec, len, sft, out, plane, L, vpad, vmax, mode, MP, st)
+    if (d.dbl) {
+        if (d.cplx) { if (is_A) OZ2_LE(double, true, true); else OZ2_LE(double, true, false); }
+        else OZ2_LE(double, false, false);
+    } else {
+        if (d.cplx) { if (is_A) OZ2_LE(float, true, true); else OZ2_LE(float, true, false); }
+        else OZ2_LE(float, false, false);
+    }
+#undef OZ2_LE
+}
+
+void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
+                             hipStream_t st) {
+    finalize_accurate_sft_kernel<<<dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, st>>>(sft0, bound, nvec, log2M, out);
+}
+
+}  // namespace oz2

@@ -1,0 +1,172 @@
+"""gemmul8 -- Python host binding of the MI355X-native Ozaki-scheme-II GEMM emulator.
+
+Thin ctypes layer over the C ABI in ``include/gemmul8_c.h`` (libgemmul8_amd.so,
+built in-tree by ``make -C mixed-gemmul8_amd``).  Mirrors the reference C++ API
+(GEMMul8/include/gemmul8.hpp:7-287): ``workSize`` and ``gemm`` with the same
+argument meaning (column-major device operands, leading dimensions, host
+alpha/beta, caller-owned workspace), plus ``matmul`` for row-major torch tensors.
+PyTorch is used only for device memory and streams.
+
+There is no CPU fallback: importing this module on a machine without the built
+library raises, and every call goes to the HIP kernels.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgemmul8_amd.so")
+
+REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, COMPLEX_CLASSIC_MULT, COMPLEX_KARATSUBA_MULT = 0, 1, 2, 3
+OP_N, OP_T, OP_C = 0, 1, 2
+R_64F, R_32F, C_64F, C_32F = 0, 1, 2, 3
+_DTYPE = {torch.float64: R_64F, torch.float32: R_32F, torch.complex128: C_64F, torch.complex64: C_32F}
+_ERR = {-1: "num_moduli outside [2, 20]", -2: "unsupported dtype combination for computeType",
+        -3: "unsupported transpose op", -4: "size limit (k beyond 2^17 or leading dimension too small)",
+        -5: "mode not implemented in this build", -6: "HIP launch failure"}
+
+
+class Gemmul8Error(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"gemmul8: native library not built ({LIB_PATH}); run `make -C mixed-gemmul8_amd`")
+    lib = ctypes.CDLL(LIB_PATH)
+    p, sz, u, i, d = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int, ctypes.POINTER(ctypes.c_double)
+    lib.gemmul8_work_size.restype = sz
+    lib.gemmul8_work_size.argtypes = [sz, sz, sz, u, i]
+    lib.gemmul8_gemm.restype = i
+    lib.gemmul8_gemm.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, p, sz, p, sz, p, p, sz, u, i, p, i, d]
+    lib.gemmul8_timing_enable.argtypes = [i]
+    lib.gemmul8_timing_read.argtypes = [d, ctypes.POINTER(ctypes.c_int)]
+    lib.gemmul8_layout.argtypes = [sz, sz, sz, u, i, ctypes.POINTER(ctypes.c_size_t)]
+    lib.gemmul8_i8_product_raw.argtypes = [p, sz, sz, sz, u, i, p, p]
+    lib.gemmul8_randmat.argtypes = [p, i, sz, sz, p, ctypes.c_double, ctypes.c_ulonglong]
+    lib.gemmul8_dd_gemm.argtypes = [p, sz, sz, sz, p, p, p, p]
+    lib.gemmul8_relerr_dd.argtypes = [p, sz, p, p, p, p]
+    return lib
+
+
+lib = _load()
+
+
+def _stream(stream=None):
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return ctypes.c_void_p(stream.cuda_stream)
+
+
+def _check(rc):
+    if rc != 0:
+        raise Gemmul8Error(f"gemmul8 error {rc}: {_ERR.get(rc, 'unknown')}")
+
+
+def _scalar(x, dtype):
+    """host alpha/beta buffer of the output type"""
+    import numpy as np
+    npt = {torch.float64: np.float64, torch.float32: np.float32, torch.complex128: np.complex128,
+           torch.complex64: np.complex64}[dtype]
+    return np.array([x], dtype=npt)
+
+
+def workSize(m, n, k, num_moduli, computeType=REAL_DEFAULT):
+    """Bytes of device workspace for gemm (gemmul8.hpp:18-22)."""
+    return int(lib.gemmul8_work_size(m, n, k, num_moduli, computeType))
+
+
+def layout(m, n, k, num_moduli, computeType=REAL_DEFAULT):
+    out = (ctypes.c_size_t * 16)()
+    lib.gemmul8_layout(m, n, k, num_moduli, computeType, out)
+    keys = ["m_pad", "n_pad", "k_pad", "ksteps", "planeA", "planeB", "planeR", "offA", "offB", "offR", "offSftA",
+            "offSftB", "offBound", "offSft0", "total", "kblk"]
+    return dict(zip(keys, list(out)))
+
+
+def gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fastmode, work,
+         computeType=REAL_DEFAULT, stream=None, phase_times=False):
+    """C = alpha*op(A)*op(B) + beta*C on column-major device buffers (gemmul8.hpp:29-47).
+
+    A, B, C, work: torch tensors (storage in column-major order, ld in elements).
+    Returns the 4 phase times in ns when phase_times=True (synchronising), else None.
+    """
+    ta, tb, tc = _DTYPE[A.dtype], _DTYPE[B.dtype], _DTYPE[C.dtype]
+    al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
+    pt = (ctypes.c_double * 4)() if phase_times else None
+    rc = lib.gemmul8_gemm(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ctypes.data, A.data_ptr(), lda,
+                          B.data_ptr(), ldb, be.ctypes.data, C.data_ptr(), ldc, num_moduli, int(bool(fastmode)),
+                          work.data_ptr(), computeType, pt)
+    _check(rc)
+    return list(pt) if phase_times else None
+
+
+def alloc_work(m, n, k, num_moduli, computeType=REAL_DEFAULT, device="cuda"):
+    return torch.empty(workSize(m, n, k, num_moduli, computeType), dtype=torch.uint8, device=device)
+
+
+def matmul(A, B, num_moduli=14, fastmode=True, out_dtype=None, work=None):
+    """Row-major torch convenience: returns A @ B emulated with num_moduli int8 products.
+
+    A row-major (m x k) tensor is a column-major k x m matrix, so the call uses
+    op T on both operands and needs no copies."""
+    assert A.is_cuda and B.is_cuda and A.dim() == 2 and B.dim() == 2 and A.shape[1] == B.shape[0]
+    A = A.contiguous()
+    B = B.contiguous()
+    m, k = A.shape
+    n = B.shape[1]
+    out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
+    cplx = A.is_complex()
+    ct = COMPLEX_BIG_MATRIX_ENCODE if cplx else REAL_DEFAULT
+    Ct = torch.empty((n, m), dtype=out_dtype, device=A.device)  # column-major m x n
+    if work is None:
+        work = alloc_work(m, n, k, num_moduli, ct, A.device)
+    if cplx:
+        # complex big-matrix encode supports op N only: materialise column-major operands
+        Acm = A.t().contiguous()
+        Bcm = B.t().contiguous()
+        gemm(OP_N, OP_N, m, n, k, 1.0, Acm, m, Bcm, k, 0.0, Ct, m, num_moduli, fastmode, work, ct)
+    else:
+        gemm(OP_T, OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, num_moduli, fastmode, work, ct)
+    return Ct.t()
+
+
+# ---- instrumentation ----
+def timing_enable(on=True):
+    lib.gemmul8_timing_enable(1 if on else 0)
+
+
+def timing_read():
+    ms = (ctypes.c_double * 4)()
+    calls = ctypes.c_int(0)
+    lib.gemmul8_timing_read(ms, ctypes.byref(calls))
+    return list(ms), calls.value
+
+
+# ---- harness (reference test-driver semantics) ----
+def randmat(m, n, dtype=torch.float64, phi=0.5, seed=123456, device="cuda", stream=None):
+    """Column-major m x n matrix (returned as an (n, m) row-major tensor) from make_matrix.hpp:8-71."""
+    X = torch.empty((n, m), dtype=dtype, device=device)
+    _check(lib.gemmul8_randmat(_stream(stream), _DTYPE[dtype], m, n, X.data_ptr(), phi, seed))
+    return X
+
+
+def dd_gemm(Acm, Bcm, m, n, k, stream=None):
+    """double-double reference of column-major A (m x k) * B (k x n); returns (C1, C2) column-major."""
+    C1 = torch.empty((n, m), dtype=torch.float64, device=Acm.device)
+    C2 = torch.empty_like(C1)
+    _check(lib.gemmul8_dd_gemm(_stream(stream), m, n, k, Acm.data_ptr(), Bcm.data_ptr(), C1.data_ptr(),
+                               C2.data_ptr()))
+    return C1, C2
+
+
+def relerr_dd(C, C1, C2, stream=None):
+    """elementwise |C - C1 - C2| / |C1 + C2| in double-double, returns (max, median) like eval.hpp:317-338."""
+    err = torch.empty(C1.numel(), dtype=torch.float64, device=C1.device)
+    _check(lib.gemmul8_relerr_dd(_stream(stream), C1.numel(), C.data_ptr(), C1.data_ptr(), C2.data_ptr(),
+                                 err.data_ptr()))
+    s, _ = torch.sort(err)
+    cnt = s.numel()
+    med = s[cnt // 2] if cnt & 1 else (s[cnt // 2] + s[cnt // 2 - 1]) * 0.5
+    return float(s[-1]), float(med)

@@ -474,8 +474,8 @@ static double crt_value(const uint8_t *R, size_t plane, size_t idx, unsigned N, 
  * the reference's variants are restated verbatim (inverse_scaling.hpp:417
  * beta*AB + C, :736/:763 alpha*C + AB). */
 static double epi_d(double v, double c, double al, double be, int numM1, int quirks) {
+    if (be == 0.0 && !(quirks && al != 1.0)) return al == 1.0 ? v : al * v; /* BLAS: C not read */
     if (al == 1.0) {
-        if (be == 0.0) return v;
         if (be == 1.0) return c + v;
         return quirks ? fma(be, v, c) : fma(be, c, v);
     }
@@ -483,8 +483,8 @@ static double epi_d(double v, double c, double al, double be, int numM1, int qui
     return fma(be, c, al * v);
 }
 static float epi_f(float v, float c, float al, float be, int quirks) {
+    if (be == 0.0f && !(quirks && al != 1.0f)) return al == 1.0f ? v : al * v;
     if (al == 1.0f) {
-        if (be == 0.0f) return v;
         if (be == 1.0f) return c + v;
         return quirks ? fmaf(be, v, c) : fmaf(be, c, v);
     }
@@ -518,7 +518,8 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
                 if (tc == 'z') {
                     const double *al = (const double *)alpha, *be = (const double *)beta;
                     double *Cz = (double *)C;
-                    double cr = Cz[2 * o], ci = Cz[2 * o + 1];
+                    int zb = be[0] == 0.0 && be[1] == 0.0;
+                    double cr = zb ? 0.0 : Cz[2 * o], ci = zb ? 0.0 : Cz[2 * o + 1];
                     if (al[0] == 1.0 && al[1] == 0.0 && be[0] == 0.0 && be[1] == 0.0) {
                         Cz[2 * o] = vr; Cz[2 * o + 1] = vi;
                     } else { /* alpha*v + beta*c, products fused as the GPU build does */
@@ -530,7 +531,8 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
                     const float *al = (const float *)alpha, *be = (const float *)beta;
                     float *Cc = (float *)C;
                     float fr = (float)vr, fi = (float)vi;
-                    float cr = Cc[2 * o], ci = Cc[2 * o + 1];
+                    int zb = be[0] == 0.0f && be[1] == 0.0f;
+                    float cr = zb ? 0.0f : Cc[2 * o], ci = zb ? 0.0f : Cc[2 * o + 1];
                     if (al[0] == 1.0f && al[1] == 0.0f && be[0] == 0.0f && be[1] == 0.0f) {
                         Cc[2 * o] = fr; Cc[2 * o + 1] = fi;
                     } else {

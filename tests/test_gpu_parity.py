@@ -1,0 +1,193 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle restatement.
+
+Bit-exact expectations (integer / exactly restated arithmetic):
+  * shifts sftA/sftB (fast mode: round-up norms reduced in the reference's order;
+    the only non-restated op is v_log_f32, whose effect is reported separately),
+  * every int8 slice of every modulus, including zero padding,
+  * every residue plane (the int8 products are exact),
+  * C bit-for-bit for f64/f32/complex outputs.
+"""
+import numpy as np
+import pytest
+
+from util import bits_equal, randmat_np, untile
+
+pytestmark = pytest.mark.gpu
+
+NP2T = None
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def to_dev(X):
+    """column-major numpy -> device tensor holding the same column-major bytes"""
+    torch = _torch()
+    Xf = np.asfortranarray(X)
+    return torch.from_numpy(np.ascontiguousarray(Xf.T)).cuda()
+
+
+def run_gpu(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta=0.0, C0=None):
+    torch = _torch()
+    import gemmul8 as G
+    A = np.asfortranarray(A)
+    B = np.asfortranarray(B)
+    m = A.shape[1] if opA else A.shape[0]
+    k = A.shape[0] if opA else A.shape[1]
+    n = B.shape[0] if opB else B.shape[1]
+    out_dtype = out_dtype or np.result_type(A.dtype, B.dtype)
+    cplx = np.iscomplexobj(A)
+    ct = G.COMPLEX_BIG_MATRIX_ENCODE if cplx else G.REAL_DEFAULT
+    if C0 is None:
+        C0 = np.zeros((m, n), out_dtype, order="F")
+    dA, dB, dC = to_dev(A), to_dev(B), to_dev(np.asfortranarray(C0.astype(out_dtype)))
+    ws = G.workSize(m, n, k, N, ct)
+    work = torch.full((ws,), 0xA5, dtype=torch.uint8, device="cuda")
+    G.gemm(opA, opB, m, n, k, alpha, dA, A.shape[0], dB, B.shape[0], beta, dC, m, N, fast, work, ct)
+    torch.cuda.synchronize()
+    C = np.asfortranarray(dC.cpu().numpy().T)
+    return C, work.cpu().numpy(), G.layout(m, n, k, N, ct)
+
+
+def ws_sft(wsb, L, m, n):
+    sA = wsb[L["offSftA"]:L["offSftA"] + 2 * m].view(np.int16)
+    sB = wsb[L["offSftB"]:L["offSftB"] + 2 * n].view(np.int16)
+    return sA.copy(), sB.copy()
+
+
+def ws_planes(wsb, L, N, which):
+    off, plane, vpad = (L["offA"], L["planeA"], L["m_pad"]) if which == "A" else (L["offB"], L["planeB"], L["n_pad"])
+    return [untile(wsb[off + j * plane: off + (j + 1) * plane].tobytes(), vpad, L["k_pad"]) for j in range(N)]
+
+
+def ws_residues(wsb, L, N):
+    R = wsb[L["offR"]:L["offR"] + N * L["planeR"]].reshape(N, L["n_pad"], L["m_pad"])
+    return R
+
+
+def check_full(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta=0.0, C0=None, vt=None):
+    from oracle import oracle as O
+    A = np.asfortranarray(A)
+    B = np.asfortranarray(B)
+    m = A.shape[1] if opA else A.shape[0]
+    k = A.shape[0] if opA else A.shape[1]
+    n = B.shape[0] if opB else B.shape[1]
+    cplx = np.iscomplexobj(A)
+    out_dtype = out_dtype or np.result_type(A.dtype, B.dtype)
+    C, wsb, L = run_gpu(A, B, N, fast, opA, opB, out_dtype, alpha, beta, C0)
+    A8o, B8o, sAo, sBo = O.scaling(A, B, N, fast, opA, opB, vt)
+    sA, sB = ws_sft(wsb, L, m, n)
+    agree_A = float(np.mean(sA == sAo)) if m else 1.0
+    agree_B = float(np.mean(sB == sBo)) if n else 1.0
+    assert agree_A == 1.0 and agree_B == 1.0, (agree_A, agree_B, np.nonzero(sA != sAo), np.nonzero(sB != sBo))
+    # slices (with the complex imaginary block at kblk instead of k) and zero padding
+    kblk = L["kblk"]
+    for which, X8o, vpad, nv in (("A", A8o, L["m_pad"], (2 * m if cplx else m)), ("B", B8o, L["n_pad"], n)):
+        planes = ws_planes(wsb, L, N, which)
+        for j in range(N):
+            P = planes[j]
+            exp = np.zeros((vpad, L["k_pad"]), np.int8)
+            if cplx:
+                exp[:nv, :k] = X8o[j][:, :k]
+                exp[:nv, kblk:kblk + k] = X8o[j][:, k:]
+            else:
+                exp[:nv, :k] = X8o[j]
+            assert np.array_equal(P, exp), f"{which} slice mismatch modulus {j}: {np.argwhere(P != exp)[:5]}"
+    R = ws_residues(wsb, L, N)
+    Ro = O.residues(A8o, B8o)
+    mr = 2 * m if cplx else m
+    assert np.array_equal(R[:, :n, :mr], Ro), "residue mismatch"
+    Co = O.gemm(A, B, N, fast, out_dtype, alpha, beta, C0, opA, opB, vt)
+    assert bits_equal(C, Co), f"C mismatch: max |diff| {np.max(np.abs(C - Co))}"
+    return C, Co
+
+
+@pytest.mark.parametrize("m,n,k", [(16, 16, 16), (33, 47, 100), (256, 256, 256), (300, 260, 513), (1, 1, 1)])
+@pytest.mark.parametrize("N", [2, 7, 8, 14, 20])
+def test_dgemm_fast(m, n, k, N):
+    rng = np.random.default_rng(1000 * m + n + k + N)
+    check_full(randmat_np(rng, m, k), randmat_np(rng, k, n), N)
+
+
+@pytest.mark.parametrize("N", [4, 8, 13, 19])
+def test_sgemm_fast(N):
+    rng = np.random.default_rng(N)
+    check_full(randmat_np(rng, 130, 77, dtype=np.float32), randmat_np(rng, 77, 90, dtype=np.float32), N)
+
+
+@pytest.mark.parametrize("N", [8, 10, 14])
+def test_mixed_accurate(N):
+    rng = np.random.default_rng(7 + N)
+    A = randmat_np(rng, 200, 150)
+    B = randmat_np(rng, 150, 120, dtype=np.float32)
+    check_full(A, B, N, fast=False)
+    check_full(B.T.copy().astype(np.float32), A.T.copy(), N, fast=False)
+
+
+@pytest.mark.parametrize("N", [6, 12])
+def test_zgemm_bigmatrix(N):
+    rng = np.random.default_rng(55 + N)
+    check_full(randmat_np(rng, 70, 90, dtype=np.complex128), randmat_np(rng, 90, 60, dtype=np.complex128), N)
+
+
+def test_cgemm_mixed_complex():
+    rng = np.random.default_rng(3)
+    check_full(randmat_np(rng, 40, 50, dtype=np.complex64), randmat_np(rng, 50, 30, dtype=np.complex128), 9,
+               out_dtype=np.complex128)
+
+
+@pytest.mark.parametrize("opA,opB", [(0, 1), (1, 0), (1, 1)])
+def test_transposes(opA, opB):
+    rng = np.random.default_rng(11)
+    m, n, k = 90, 70, 110
+    A = randmat_np(rng, k, m) if opA else randmat_np(rng, m, k)
+    B = randmat_np(rng, n, k) if opB else randmat_np(rng, k, n)
+    check_full(A, B, 14, opA=opA, opB=opB)
+    check_full(A, B, 10, fast=False, opA=opA, opB=opB)
+
+
+@pytest.mark.parametrize("alpha,beta", [(1.0, 1.0), (2.5, 0.0), (1.0, -0.5), (-1.5, 1.0), (0.75, 2.0)])
+def test_alpha_beta(alpha, beta):
+    rng = np.random.default_rng(21)
+    A, B = randmat_np(rng, 64, 80), randmat_np(rng, 80, 48)
+    C0 = randmat_np(rng, 64, 48)
+    check_full(A, B, 14, alpha=alpha, beta=beta, C0=C0)
+    check_full(A.astype(np.float32), B.astype(np.float32), 8, alpha=alpha, beta=beta, C0=C0.astype(np.float32))
+
+
+def test_zero_rows_and_cols():
+    rng = np.random.default_rng(5)
+    A, B = randmat_np(rng, 50, 60), randmat_np(rng, 60, 40)
+    A[3, :] = 0
+    B[:, 7] = 0
+    C, _ = check_full(A, B, 14)
+    assert np.all(C[3, :] == 0) and np.all(C[:, 7] == 0)
+
+
+def test_mfma_raw_product():
+    """v_mfma_i32_32x32x32_i8 tile/epilogue mapping: exact int32 product of random int8 planes."""
+    torch = _torch()
+    import gemmul8 as G
+    from util import tile
+    rng = np.random.default_rng(9)
+    m, n, k, N = 300, 520, 200, 2
+    L = G.layout(m, n, k, N)
+    A8 = np.zeros((L["m_pad"], L["k_pad"]), np.int8)
+    B8 = np.zeros((L["n_pad"], L["k_pad"]), np.int8)
+    A8[:m, :k] = rng.integers(-128, 128, (m, k))
+    B8[:n, :k] = rng.integers(-128, 128, (n, k))
+    ws = np.zeros(L["total"], np.uint8)
+    ws[L["offA"]:L["offA"] + L["planeA"]] = tile(A8, L["m_pad"], L["k_pad"]).view(np.uint8)
+    ws[L["offB"]:L["offB"] + L["planeB"]] = tile(B8, L["n_pad"], L["k_pad"]).view(np.uint8)
+    work = torch.from_numpy(ws).cuda()
+    C32 = torch.zeros((L["n_pad"], L["m_pad"]), dtype=torch.int32, device="cuda")
+    import ctypes
+    rc = G.lib.gemmul8_i8_product_raw(G._stream(), m, n, k, N, 0, ctypes.c_void_p(work.data_ptr()),
+                                      ctypes.c_void_p(C32.data_ptr()))
+    assert rc == 0
+    torch.cuda.synchronize()
+    got = C32.cpu().numpy().T  # (m_pad, n_pad)
+    exp = A8.astype(np.int64) @ B8.astype(np.int64).T
+    assert np.array_equal(got, exp)
