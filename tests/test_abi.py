@@ -1,0 +1,66 @@
+"""The drop-in boundary: libgemmul8_amd.so loads and exports every C entry point declared in
+include/gemmul8_c.h, and every C++ symbol of the reference library (identical mangled names, so
+objects compiled against the reference's gemmul8.hpp link unchanged).  No GPU needed."""
+import ctypes
+import os
+import re
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "mixed-gemmul8_amd", "gemmul8", "libgemmul8_amd.so")
+
+
+def _declared_c_functions():
+    txt = open(os.path.join(ROOT, "include", "gemmul8_c.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(gemmul8_[a-z0-9_]+)\s*\(", txt)))
+
+
+def _exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_library_loads():
+    assert os.path.exists(LIB), "build first: make -C mixed-gemmul8_amd"
+    ctypes.CDLL(LIB)
+
+
+def test_c_abi_exports_every_declared_function():
+    decl = _declared_c_functions()
+    assert len(decl) >= 9
+    exp = _exported()
+    missing = [f for f in decl if f not in exp]
+    assert not missing, missing
+
+
+def test_cpp_symbols_match_reference():
+    ref = open(os.path.join(ROOT, "tests", "golden", "ref_symbols.txt")).read().split()
+    exp = _exported()
+    missing = [s for s in ref if s not in exp]
+    assert not missing, missing
+    assert any("gemmIdddE" in s for s in ref)
+
+
+def test_work_size_and_errors_host_only():
+    lib = ctypes.CDLL(LIB)
+    lib.gemmul8_work_size.restype = ctypes.c_size_t
+    lib.gemmul8_work_size.argtypes = [ctypes.c_size_t] * 3 + [ctypes.c_uint, ctypes.c_int]
+    ws = lib.gemmul8_work_size(8192, 8192, 8192, 14, 0)
+    # 14 planes of A and B slices + 14 residue planes + shifts (layout in csrc/oz2_common.hpp)
+    assert ws >= 14 * (2 * 8192 * 8192 + 8192 * 8192)
+    assert lib.gemmul8_work_size(8192, 8192, 8192, 14, 7) == 0  # unknown compute type (gemmul8.cu:142-145)
+    lib.gemmul8_gemm.restype = ctypes.c_int
+    # invalid arguments are rejected before anything touches the device
+    p = ctypes.c_void_p
+    lib.gemmul8_gemm.argtypes = [p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                 ctypes.c_int, ctypes.c_int, ctypes.c_int, p, p, ctypes.c_size_t, p, ctypes.c_size_t,
+                                 p, p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int, p, ctypes.c_int, p]
+    args = lambda N, ta=0, tb=0, tc=0, ct=0, k=8: (None, 0, 0, 8, 8, k, ta, tb, tc, None, None, 8, None, k, None,
+                                                    None, 8, N, 1, None, ct, None)
+    assert lib.gemmul8_gemm(*args(1)) == -1
+    assert lib.gemmul8_gemm(*args(21)) == -1
+    assert lib.gemmul8_gemm(*args(14, ta=2)) == -2          # complex A with real B
+    assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2)) == -2  # complex types need COMPLEX_BIG_MATRIX_ENCODE
+    assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2, ct=3)) == -5  # Karatsuba: not in this build
+    assert lib.gemmul8_gemm(*args(14, k=(1 << 17) + 1)) == -4
