@@ -1,0 +1,94 @@
+"""Live parity against the REFERENCE's own HIP build (oracle/_ref, compiled from the unmodified
+/root/reference sources by oracle/ref/Makefile) on the same device inputs, up to the full
+BASELINE size (cfg2: 8192^3, 14 moduli).  Expectation: C bit-identical.
+
+Also records both implementations' wall time per call into gpurun_out/ref_compare.json
+(the reference's own 4 phase timers include its device-wide syncs)."""
+import ctypes
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.path.join(ROOT, "oracle", "_ref", "libgemmul8_ref.so")
+RESULTS = {}
+
+
+def _ref():
+    if not os.path.exists(REF):
+        pytest.skip("oracle/_ref not built (needs /root/reference at build time)")
+    lib = ctypes.CDLL(REF)
+    p, sz, i, u = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint
+    lib.ref_gemm.argtypes = [i, i, i, i, i, sz, sz, sz, p, p, sz, p, sz, p, p, sz, u, i, i, p, p]
+    lib.ref_work_size.restype = sz
+    lib.ref_work_size.argtypes = [sz, sz, sz, u, i]
+    return lib
+
+
+CODES = {"d": 0, "s": 1, "z": 2, "c": 3}
+
+
+@pytest.mark.parametrize("case", [
+    ("d", "d", "d", 1024, 1024, 1024, 14, 1),
+    ("d", "d", "d", 1000, 700, 1500, 8, 1),
+    ("s", "s", "s", 1024, 768, 2048, 6, 1),
+    ("d", "s", "d", 2048, 1536, 1000, 10, 0),
+    ("d", "d", "d", 1536, 1024, 2048, 14, 0),
+    ("z", "z", "z", 512, 640, 384, 12, 1),
+    ("d", "d", "d", 8192, 8192, 8192, 14, 1),
+])
+def test_same_inputs_same_bits(case):
+    import torch
+    import gemmul8 as G
+    ta, tb, tc, m, n, k, N, fast = case
+    lib = _ref()
+    tdt = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}
+    A = G.randmat(m, k, tdt[ta], 0.5, 123456)
+    B = G.randmat(k, n, tdt[tb], 0.5, 123456)
+    ct = 1 if tc in "zc" else 0
+    C_ref = torch.zeros((n, m), dtype=tdt[tc], device="cuda")
+    C_new = torch.zeros_like(C_ref)
+    npt = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}[tc]
+    one, zero = np.array([1], npt), np.array([0], npt)
+    wref = torch.zeros(lib.ref_work_size(m, n, k, N, ct) + 16 * A.numel() + (1 << 20), dtype=torch.uint8,
+                       device="cuda")
+    wnew = G.alloc_work(m, n, k, N, ct)
+
+    def run_ref():
+        rc = lib.ref_gemm(CODES[ta], CODES[tb], CODES[tc], 0, 0, m, n, k, one.ctypes.data, A.data_ptr(), m,
+                          B.data_ptr(), k, zero.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
+        assert rc == 0
+
+    def run_new():
+        G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C_new, m, N, bool(fast), wnew, ct)
+
+    run_ref()
+    run_new()
+    torch.cuda.synchronize()
+    same = torch.equal(C_ref, C_new)
+    nbad = int((C_ref != C_new).sum().item())
+    # timing (median of a few calls each, after the warm-up above)
+    tt = {}
+    for name, fn in (("reference", run_ref), ("mi355x", run_new)):
+        ts = []
+        for _ in range(3 if m * n * k > 1e11 else 5):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        tt[name] = float(np.median(ts))
+    mult = 8 if ct else 2
+    RESULTS["%s%s%s_%dx%dx%d_N%d_%s" % (ta, tb, tc, m, n, k, N, "fast" if fast else "accu")] = {
+        "bit_identical": bool(nbad == 0), "n_diff": nbad,
+        "ref_ms": tt["reference"] * 1e3, "mi355x_ms": tt["mi355x"] * 1e3,
+        "ref_tflops": mult * m * n * k / tt["reference"] / 1e12, "mi355x_tflops": mult * m * n * k / tt["mi355x"] / 1e12}
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "ref_compare.json"), "w") as f:
+        json.dump(RESULTS, f, indent=1)
+    assert same and nbad == 0, f"{nbad} elements differ from the reference"
