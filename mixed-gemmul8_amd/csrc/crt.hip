@@ -5,13 +5,18 @@
 // then the BLAS epilogue.  Operation order restates
 // GEMMul8/src/inverse_scaling.hpp:35-62 (numM = 1) and :138-172 (numM = 2), so
 // the result is bit-identical to the reference for the same residues.
-// Each thread reads one 4-byte word from every residue plane (4 consecutive rows
-// of one column, coalesced across the wave) and writes 4 consecutive outputs;
-// the weights arrive as kernel arguments (the reference uploads them to
-// __constant__ on every call, gemmul8.cu:236-241).
+//
+// HBM-bound streaming kernel: each thread owns 8 consecutive rows of one column,
+// reads one 8-byte word from each of the N residue planes (coalesced across the
+// wave: 512 B per plane per wave instruction) and writes 8 outputs.  N is a
+// template parameter (19 instantiations) so every plane load is unguarded and
+// the accumulation fully unrolled; the weights arrive as kernel arguments (the
+// reference uploads them to __constant__ on every call, gemmul8.cu:236-241).
 #include "oz2_split.hpp"
 
 namespace oz2 {
+
+constexpr int CRT_ROWS = 8;
 
 struct CrtArgs {
     const uint8_t *R;
@@ -25,25 +30,20 @@ struct CrtArgs {
     CrtParams cp;
 };
 
-template <bool NUMM1>
-__device__ __forceinline__ double crt_value(const CrtParams &cp, const uint32_t *w, int e) {
-    const unsigned N = cp.N;
-    // loops are unrolled to OZ2_MAX_MODULI with a uniform guard so w[] stays in VGPRs
+template <unsigned N, bool NUMM1>
+__device__ __forceinline__ double crt_value(const CrtParams &cp, const uint8_t (&r)[N]) {
     if (NUMM1) {
         double C = 0.0;
 #pragma unroll
-        for (unsigned i = 0; i < OZ2_MAX_MODULI; ++i)
-            if (i < N) C = __builtin_fma(cp.w_hi[i], (double)((w[i] >> (8 * e)) & 0xffu), C);
+        for (unsigned i = 0; i < N; ++i) C = __builtin_fma(cp.w_hi[i], (double)r[i], C);
         const double quot = -__builtin_rint(C * cp.invM);
         return __builtin_fma(quot, cp.M1, C);
     } else {
         double C1 = 0.0, C2 = 0.0;
 #pragma unroll
-        for (unsigned i = 0; i < OZ2_MAX_MODULI; ++i) {
-            if (i >= N) break;
-            const double r = (double)((w[i] >> (8 * e)) & 0xffu);
-            C1 = __builtin_fma(cp.w_hi[i], r, C1);
-            C2 = __builtin_fma(cp.w_lo[i], r, C2);
+        for (unsigned i = 0; i < N; ++i) {
+            C1 = __builtin_fma(cp.w_hi[i], (double)r[i], C1);
+            C2 = __builtin_fma(cp.w_lo[i], (double)r[i], C2);
         }
         const double quot = -__builtin_rint(__builtin_fma(C1, cp.invM, C2 * cp.invM));
         const double t1 = __builtin_fma(quot, cp.M1, C1) + C2;
@@ -51,19 +51,17 @@ __device__ __forceinline__ double crt_value(const CrtParams &cp, const uint32_t 
     }
 }
 
-__device__ __forceinline__ void load_words(const CrtArgs &a, size_t off, bool aligned, size_t rows_left, uint32_t *w) {
-    const unsigned N = a.cp.N;
-    if (aligned && rows_left >= 4) {
+// residues of rows [off, off+8) of every plane; the fast path is one 8-byte load per plane
+template <unsigned N>
+__device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fast, int nr, uint64_t (&w)[N]) {
+    if (fast) {
 #pragma unroll
-        for (unsigned i = 0; i < OZ2_MAX_MODULI; ++i)
-            w[i] = i < N ? *reinterpret_cast<const uint32_t *>(a.R + i * a.planeR + off) : 0u;
+        for (unsigned i = 0; i < N; ++i) w[i] = *reinterpret_cast<const uint64_t *>(a.R + i * a.planeR + off);
     } else {
 #pragma unroll
-        for (unsigned i = 0; i < OZ2_MAX_MODULI; ++i) {
-            if (i >= N) { w[i] = 0; continue; }
-            uint32_t x = 0;
-            for (int e = 0; e < 4; ++e)
-                if ((size_t)e < rows_left) x |= (uint32_t)a.R[i * a.planeR + off + e] << (8 * e);
+        for (unsigned i = 0; i < N; ++i) {
+            uint64_t x = 0;
+            for (int e = 0; e < nr; ++e) x |= (uint64_t)a.R[i * a.planeR + off + e] << (8 * e);
             w[i] = x;
         }
     }
@@ -90,62 +88,141 @@ __device__ __forceinline__ float epi_f(float v, float c, float al, float be) {
     return __builtin_fmaf(be, c, al * v);
 }
 
-template <int OT, bool NUMM1>
+// intra-wave LDS handoff (the whole wave takes part; no block-level barrier is needed)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int OT> struct OutElem;
+template <> struct OutElem<0> { using T = double; };
+template <> struct OutElem<1> { using T = float; };
+template <> struct OutElem<2> { using T = double2; };
+template <> struct OutElem<3> { using T = float2; };
+
+template <int OT> struct BlasEpi;
+template <> struct BlasEpi<0> {
+    static __device__ __forceinline__ double f(double v, double c, const CrtArgs &a) { return epi_d(v, c, a.ar, a.br); }
+};
+template <> struct BlasEpi<1> {
+    static __device__ __forceinline__ float f(float v, float c, const CrtArgs &a) {
+        return epi_f(v, c, (float)a.ar, (float)a.br);
+    }
+};
+template <> struct BlasEpi<2> {
+    static __device__ __forceinline__ double2 f(double2 v, double2 c, const CrtArgs &a) {
+        const double tr = __builtin_fma(a.ar, v.x, -a.ai * v.y), ti = __builtin_fma(a.ar, v.y, a.ai * v.x);
+        return make_double2(__builtin_fma(a.br, c.x, __builtin_fma(-a.bi, c.y, tr)),
+                            __builtin_fma(a.br, c.y, __builtin_fma(a.bi, c.x, ti)));
+    }
+};
+template <> struct BlasEpi<3> {
+    static __device__ __forceinline__ float2 f(float2 v, float2 c, const CrtArgs &a) {
+        const float arf = (float)a.ar, aif = (float)a.ai, brf = (float)a.br, bif = (float)a.bi;
+        const float tr = __builtin_fmaf(arf, v.x, -aif * v.y), ti = __builtin_fmaf(arf, v.y, aif * v.x);
+        return make_float2(__builtin_fmaf(brf, c.x, __builtin_fmaf(-bif, c.y, tr)),
+                           __builtin_fmaf(brf, c.y, __builtin_fmaf(bif, c.x, ti)));
+    }
+};
+
+// One wave covers 512 consecutive rows of a column: lane l recombines rows 8l..8l+7
+// (one 8-byte load per plane), parks the scaled values in LDS, and the wave then
+// writes them back as 16-byte vectors in lane order so the C stream (the larger
+// one) is fully coalesced.  The BLAS epilogue runs after the transpose, on the
+// coalesced C read when beta != 0.
+template <int OT, bool NUMM1, unsigned N>
 __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
-    const size_t r0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (r0 >= a.m) return;
-    const size_t rows_left = a.m - r0;
-    const int nr = rows_left >= 4 ? 4 : (int)rows_left;
-    for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
-        uint32_t w[OZ2_MAX_MODULI], wi[OZ2_MAX_MODULI];
-        const size_t off = col * a.ldr + r0;
-        load_words(a, off, true, rows_left, w);
-        if (OT >= 2) load_words(a, off + a.imag_off, (a.imag_off & 3) == 0, rows_left, wi);
-        const int sB = a.sftB[col];
+    using E = typename OutElem<OT>::T;
+    constexpr int EPV = 16 / sizeof(E);  // elements per 16-byte vector
+    __shared__ E buf[4][64 * CRT_ROWS];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const size_t wrow0 = ((size_t)blockIdx.x * 256 + wv * 64) * CRT_ROWS;
+    if (wrow0 >= a.m) return;  // whole wave beyond the last row (no block-level sync below)
+    const size_t r0 = wrow0 + (size_t)lane * CRT_ROWS;
+    const int nr = r0 >= a.m ? 0 : (a.m - r0 >= CRT_ROWS ? CRT_ROWS : (int)(a.m - r0));
+    const bool plain_ab = a.ar == 1.0 && a.ai == 0.0 && a.br == 0.0 && a.bi == 0.0;
+    const bool zero_beta = a.br == 0.0 && a.bi == 0.0;
+    int16_t sa[CRT_ROWS];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if (e < nr) {
-            const size_t row = r0 + e;
-            const int sft = (int)a.sftA[row] + sB;
-            const double vr = scalbn(crt_value<NUMM1>(a.cp, w, e), sft);
-            const size_t o = col * a.ldc + row;
-            if (OT == 0) {
-                double *C = static_cast<double *>(a.C);
-                C[o] = epi_d(vr, a.br == 0.0 ? 0.0 : C[o], a.ar, a.br);
-            } else if (OT == 1) {
-                float *C = static_cast<float *>(a.C);
-                const float al = (float)a.ar, be = (float)a.br;
-                C[o] = epi_f(__double2float_rn(vr), be == 0.0f ? 0.0f : C[o], al, be);
-            } else {
-                const double vi = scalbn(crt_value<NUMM1>(a.cp, wi, e), sft);
-                const bool plain = a.ar == 1.0 && a.ai == 0.0 && a.br == 0.0 && a.bi == 0.0;
-                const bool zb = a.br == 0.0 && a.bi == 0.0;
-                if (OT == 2) {
-                    double2 *C = static_cast<double2 *>(a.C);
-                    if (plain) {
-                        C[o] = make_double2(vr, vi);
-                    } else {
-                        const double2 c = zb ? make_double2(0.0, 0.0) : C[o];
-                        const double tr = __builtin_fma(a.ar, vr, -a.ai * vi), ti = __builtin_fma(a.ar, vi, a.ai * vr);
-                        C[o] = make_double2(__builtin_fma(a.br, c.x, __builtin_fma(-a.bi, c.y, tr)),
-                                            __builtin_fma(a.br, c.y, __builtin_fma(a.bi, c.x, ti)));
-                    }
+    for (int e = 0; e < CRT_ROWS; ++e) sa[e] = e < nr ? a.sftA[r0 + e] : 0;
+    E *wb = buf[wv];
+    for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
+        const int sB = a.sftB[col];
+        if (nr > 0) {
+            uint64_t w[N], wi[N];
+            const size_t off = col * a.ldr + r0;
+            load_rows<N>(a, off, nr == CRT_ROWS, nr, w);
+            if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == CRT_ROWS && (a.imag_off & 7) == 0, nr, wi);
+#pragma unroll
+            for (int e = 0; e < CRT_ROWS; ++e) {
+                uint8_t r[N];
+#pragma unroll
+                for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
+                const int sft = (int)sa[e] + sB;
+                const double vr = scalbn(crt_value<N, NUMM1>(a.cp, r), sft);
+                if constexpr (OT == 0) {
+                    wb[lane * CRT_ROWS + e] = vr;
+                } else if constexpr (OT == 1) {
+                    wb[lane * CRT_ROWS + e] = __double2float_rn(vr);
                 } else {
-                    float2 *C = static_cast<float2 *>(a.C);
-                    const float fr = __double2float_rn(vr), fi = __double2float_rn(vi);
-                    if (plain) {
-                        C[o] = make_float2(fr, fi);
+#pragma unroll
+                    for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(wi[i] >> (8 * e));
+                    const double vi = scalbn(crt_value<N, NUMM1>(a.cp, r), sft);
+                    if constexpr (OT == 2) wb[lane * CRT_ROWS + e] = make_double2(vr, vi);
+                    else wb[lane * CRT_ROWS + e] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
+                }
+            }
+        }
+        wave_sync();
+        E *Cc = static_cast<E *>(a.C) + col * a.ldc + wrow0;
+        const bool vec_ok = (reinterpret_cast<uintptr_t>(Cc) & 15) == 0;
+#pragma unroll
+        for (int j = 0; j < CRT_ROWS / EPV; ++j) {
+            const int idx = j * 64 * EPV + lane * EPV;
+            E v[EPV];
+            *reinterpret_cast<int4 *>(v) = *reinterpret_cast<const int4 *>(wb + idx);
+            if (vec_ok && wrow0 + idx + EPV <= a.m) {
+                if (!plain_ab) {
+                    E c[EPV];
+                    if (zero_beta) {
+#pragma unroll
+                        for (int q = 0; q < EPV; ++q) c[q] = E{};
                     } else {
-                        const float2 c = zb ? make_float2(0.0f, 0.0f) : C[o];
-                        const float arf = (float)a.ar, aif = (float)a.ai, brf = (float)a.br, bif = (float)a.bi;
-                        const float tr = __builtin_fmaf(arf, fr, -aif * fi), ti = __builtin_fmaf(arf, fi, aif * fr);
-                        C[o] = make_float2(__builtin_fmaf(brf, c.x, __builtin_fmaf(-bif, c.y, tr)),
-                                           __builtin_fmaf(brf, c.y, __builtin_fmaf(bif, c.x, ti)));
+                        *reinterpret_cast<int4 *>(c) = *reinterpret_cast<const int4 *>(Cc + idx);
+                    }
+#pragma unroll
+                    for (int q = 0; q < EPV; ++q) v[q] = BlasEpi<OT>::f(v[q], c[q], a);
+                }
+                *reinterpret_cast<int4 *>(Cc + idx) = *reinterpret_cast<const int4 *>(v);
+            } else {
+#pragma unroll
+                for (int q = 0; q < EPV; ++q) {
+                    if (wrow0 + idx + q < a.m) {
+                        E x = v[q];
+                        if (!plain_ab) x = BlasEpi<OT>::f(x, zero_beta ? E{} : Cc[idx + q], a);
+                        Cc[idx + q] = x;
                     }
                 }
             }
-            }
         }
+        wave_sync();
+    }
+}
+
+template <int OT, bool NUMM1, unsigned N>
+static void launch_crt_n(const CrtArgs &a, dim3 grid, hipStream_t st) {
+    crt_kernel<OT, NUMM1, N><<<grid, dim3(256), 0, st>>>(a);
+}
+
+template <int OT, bool NUMM1>
+static void launch_crt(const CrtArgs &a, unsigned N, dim3 grid, hipStream_t st) {
+    switch (N) {
+#define OZ2_N(n) case n: launch_crt_n<OT, NUMM1, n>(a, grid, st); break;
+        OZ2_N(2) OZ2_N(3) OZ2_N(4) OZ2_N(5) OZ2_N(6) OZ2_N(7) OZ2_N(8) OZ2_N(9) OZ2_N(10) OZ2_N(11)
+        OZ2_N(12) OZ2_N(13) OZ2_N(14) OZ2_N(15) OZ2_N(16) OZ2_N(17) OZ2_N(18) OZ2_N(19) OZ2_N(20)
+#undef OZ2_N
+    default: break;
     }
 }
 
@@ -175,18 +252,16 @@ void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const i
         break;
     }
     a.cp = CP;
-    const unsigned gx = (unsigned)((L.m + 1023) / 1024);
+    const unsigned gx = (unsigned)((L.m + 256 * CRT_ROWS - 1) / (256 * CRT_ROWS));
     const unsigned gy = (unsigned)(L.n < 65535 ? L.n : 65535);
     dim3 grid(gx, gy);
-#define OZ2_CRT(ot_, nm) crt_kernel<ot_, nm><<<grid, dim3(256), 0, st>>>(a)
     const bool nm1 = CP.numM1 != 0;
     switch (ot) {
-    case OutType::F64: if (nm1) OZ2_CRT(0, true); else OZ2_CRT(0, false); break;
-    case OutType::F32: OZ2_CRT(1, true); break;
-    case OutType::C64: if (nm1) OZ2_CRT(2, true); else OZ2_CRT(2, false); break;
-    default: OZ2_CRT(3, true); break;
+    case OutType::F64: if (nm1) launch_crt<0, true>(a, CP.N, grid, st); else launch_crt<0, false>(a, CP.N, grid, st); break;
+    case OutType::F32: launch_crt<1, true>(a, CP.N, grid, st); break;
+    case OutType::C64: if (nm1) launch_crt<2, true>(a, CP.N, grid, st); else launch_crt<2, false>(a, CP.N, grid, st); break;
+    default: launch_crt<3, true>(a, CP.N, grid, st); break;
     }
-#undef OZ2_CRT
 }
 
 }  // namespace oz2

@@ -87,7 +87,18 @@ __global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ 
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const R *__restrict__ x = X + (CPLX ? 2 : 1) * v * ld;
     R amax = 0, sum = 0;
-    for (size_t e = t; e < len; e += VT) {
+    // loads are issued in unguarded batches of U ahead of the round-up chain (whose
+    // mode-register writes would otherwise serialise each load behind the previous fma)
+    constexpr int U = 8;
+    size_t e = t;
+    for (; e + (U - 1) * VT < len; e += U * VT) {
+        R re[U], im[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_elem<R, CPLX>(x, e + u * VT, re[u], im[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) accum<R, CPLX>(re[u], im[u], amax, sum);
+    }
+    for (; e < len; e += VT) {
         R re, im;
         load_elem<R, CPLX>(x, e, re, im);
         accum<R, CPLX>(re, im, amax, sum);
@@ -131,7 +142,16 @@ __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict_
     for (int c = 0; c < NA; ++c) acc[c] = 0;
     R amax = 0;
     if (v < nvec) {
-        for (size_t b = 0; b < len; b += VT) {
+        size_t b = 0;
+        // full chunks: all NA loads issued before the round-up chains consume them
+        for (; b + VT <= len; b += VT) {
+            R re[NA], im[NA];
+#pragma unroll
+            for (int c = 0; c < NA; ++c) load_elem<R, CPLX>(X, (b + slot + 16 * c) * ld + v, re[c], im[c]);
+#pragma unroll
+            for (int c = 0; c < NA; ++c) accum<R, CPLX>(re[c], im[c], amax, acc[c]);
+        }
+        for (; b < len; b += VT) {
 #pragma unroll
             for (int c = 0; c < NA; ++c) {
                 const size_t e = b + slot + 16 * c;
@@ -197,17 +217,39 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
     const int tid = threadIdx.x;
     __shared__ R tile[KT][64 + 1][NC];
 
-    // stage the tile, coalesced along whichever index is contiguous in HBM
+    // stage the tile, coalesced along whichever index is contiguous in HBM; interior tiles
+    // load without per-element guards so all loads are in flight at once
+    constexpr int NL = (64 * KT) / NT;
+    const bool interior = v0 + 64 <= nvec && e0 + KT <= len;
+    R lre[NL], lim[NL];
+    if (interior) {  // block-uniform branch: one batch of unguarded loads
 #pragma unroll
-    for (int i = 0; i < (64 * KT) / NT; ++i) {
+        for (int i = 0; i < NL; ++i) {
+            const int idx = tid + NT * i;
+            int vl, el;
+            if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
+            const size_t v = v0 + vl, e = e0 + el;
+            load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            const int idx = tid + NT * i;
+            int vl, el;
+            if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
+            const size_t v = v0 + vl, e = e0 + el;
+            lre[i] = 0;
+            lim[i] = 0;
+            if (v < nvec && e < len) load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
         const int idx = tid + NT * i;
         int vl, el;
         if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
-        const size_t v = v0 + vl, e = e0 + el;
-        R re = 0, im = 0;
-        if (v < nvec && e < len) load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, re, im);
-        tile[el][vl][0] = re;
-        if (CPLX) tile[el][vl][NC - 1] = im;
+        tile[el][vl][0] = lre[i];
+        if (CPLX) tile[el][vl][NC - 1] = lim[i];
     }
     __syncthreads();
 
