@@ -46,6 +46,29 @@ int gemmul8_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k,
                  const void *alpha, const void *A, size_t lda, const void *B, size_t ldb, const void *beta, void *C,
                  size_t ldc, unsigned num_moduli, int fastmode, void *work, int compute_type, double *phase_ns);
 
+/* --- phase entry points (multi-GPU sharding, gemmul8/dist.py) ------------------------------------
+ * gemmul8_gemm == gemmul8_split(0, N) + gemmul8_products(0, N) + gemmul8_recombine, on one stream.
+ * Splitting the moduli range lets rank r of a modulus-sharded job produce only the residue planes
+ * [mod_begin, mod_end) (plane j at work + offR + j * planeR, see gemmul8_layout); the root then
+ * receives the other planes into its own workspace and runs gemmul8_recombine.  Every rank
+ * computes the full shift vectors (they do not depend on the modulus).
+ *
+ * Accurate mode couples the shifts of op(B)'s columns to every row of op(A) (the int8 bound
+ * product's column maxima).  A row-block shard therefore runs gemmul8_split_bound, combines the
+ * column maxima (int32 [n] at work + offBound + 4 * m_pad) with a MAX all-reduce, and calls
+ * gemmul8_split with GEMMUL8_SPLIT_BOUND_READY. */
+enum { GEMMUL8_SPLIT_BOUND_READY = 1 };
+int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
+                        void *work, int compute_type);
+int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b, int type_c,
+                  const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli, int fastmode, void *work,
+                  int compute_type, unsigned mod_begin, unsigned mod_end, int flags);
+int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, void *work,
+                     unsigned mod_begin, unsigned mod_end);
+int gemmul8_recombine(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c, int compute_type,
+                      const void *alpha, const void *beta, void *C, size_t ldc, void *work);
+
 /* --- instrumentation (used by bench.py / tests) --------------------------------------------- */
 /* When enabled, every gemmul8_gemm records HIP events between its phases on its stream; the
  * accumulated per-phase milliseconds and the call count are read (and reset) with

@@ -237,7 +237,7 @@ epilogue:
     // accumulator map (32x32 fragments): col = lane & 31, row = (r & 3) + 8*(r >> 2) + 4*(lane >> 5)
     if constexpr (EPI == (int)Epi::RESIDUE) {
         const int p = g.p[j], bar = g.barrett[j];
-        const bool p256 = (j == 0);
+        const bool p256 = (p == 256);  // modulus 256: the low byte (conv_32i_2_8u.hpp:7-20)
         uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
 #pragma unroll
         for (int i = 0; i < 4; ++i)

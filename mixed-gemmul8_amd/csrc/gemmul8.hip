@@ -76,18 +76,92 @@ static void resolve_all() {
 
 static inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
 
-static int run(const Call &c, double *phase_ns) {
-    const Layout L = make_layout(c.m, c.n, c.k, c.N, c.cplx);
-    int8_t *base = static_cast<int8_t *>(c.work);
-    int8_t *A8 = base + L.offA;
-    int8_t *B8 = base + L.offB;
-    uint8_t *R = reinterpret_cast<uint8_t *>(base + L.offR);
-    int16_t *sftA = reinterpret_cast<int16_t *>(base + L.offSftA);
-    int16_t *sftB = reinterpret_cast<int16_t *>(base + L.offSftB);
-    int32_t *bound = reinterpret_cast<int32_t *>(base + L.offBound);
-    int16_t *sft0 = reinterpret_cast<int16_t *>(base + L.offSft0);
+// Workspace views of one call (layout: oz2_common.hpp make_layout)
+struct Views {
+    Layout L;
+    int8_t *A8, *B8;
+    uint8_t *R;
+    int16_t *sftA, *sftB, *sft0;
+    int32_t *bound;
+};
+static Views views(void *work, size_t m, size_t n, size_t k, unsigned N, bool cplx) {
+    Views v;
+    v.L = make_layout(m, n, k, N, cplx);
+    int8_t *base = static_cast<int8_t *>(work);
+    v.A8 = base + v.L.offA;
+    v.B8 = base + v.L.offB;
+    v.R = reinterpret_cast<uint8_t *>(base + v.L.offR);
+    v.sftA = reinterpret_cast<int16_t *>(base + v.L.offSftA);
+    v.sftB = reinterpret_cast<int16_t *>(base + v.L.offSftB);
+    v.bound = reinterpret_cast<int32_t *>(base + v.L.offBound);
+    v.sft0 = reinterpret_cast<int16_t *>(base + v.L.offSft0);
+    return v;
+}
+
+// moduli [j0, j1) of an N-moduli call, renumbered from 0 (plane pointers are offset by the caller)
+static ModParams sub_mod_params(unsigned N, unsigned j0, unsigned j1) {
+    const ModParams full = make_mod_params(N);
+    ModParams P{};
+    for (unsigned i = 0; i < j1 - j0; ++i) {
+        P.p[i] = full.p[j0 + i];
+        P.barrett[i] = full.barrett[j0 + i];
+        P.rinv_d[i] = full.rinv_d[j0 + i];
+        P.rinv_f[i] = full.rinv_f[j0 + i];
+    }
+    P.N = j1 - j0;
+    return P;
+}
+
+// accurate mode, first half of phase 1: sft0 = 5 - ilogb(amax), the 6-bit magnitude planes and the
+// bound product's row / column maxima (scaling.hpp:3053-3100)
+static void phase_bound(const Call &c, const Views &v) {
+    const Layout &L = v.L;
     const ModParams MP = make_mod_params(c.N);
-    const CrtParams CP = make_crt_params(c.N, c.ot == OutType::F32 || c.ot == OutType::C32);
+    split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
+    split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.st);
+    split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
+    split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.st);
+    (void)hipMemsetAsync(v.bound, 0, (L.m_pad + L.n_pad) * sizeof(int32_t), c.st);
+    gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
+}
+
+// phase 1: shifts of every row of op(A) / column of op(B) (all moduli share them) and the
+// slices of moduli [j0, j1) (scaling.hpp:3680-3734 fast, :3053-3136 accurate).  bound_ready:
+// accurate mode takes the row / column maxima already in the workspace (phase_bound, possibly
+// combined across row blocks by the caller).
+static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1, bool bound_ready) {
+    const Layout &L = v.L;
+    if (c.fast) {
+        const float log2M = oz2_log2M_fast[c.N - 2];
+        split_stats(c.A, c.k, c.m, c.VT, false, log2M, v.sftA, c.st);
+        split_stats(c.B, c.k, c.n, c.VT, false, log2M, v.sftB, c.st);
+    } else {
+        const float log2M = oz2_log2M_accu[c.N - 2];
+        if (!bound_ready) phase_bound(c, v);
+        split_finalize_accurate(v.sft0, v.bound, c.m, log2M, v.sftA, c.st);
+        split_finalize_accurate(v.sft0 + L.m_pad, v.bound + L.m_pad, c.n, log2M, v.sftB, c.st);
+    }
+    const ModParams SP = sub_mod_params(c.N, j0, j1);
+    split_encode(c.A, true, c.m, c.k, v.sftA, v.A8 + j0 * L.planeA, L.planeA, L, 0, SP, c.st);
+    split_encode(c.B, false, c.n, c.k, v.sftB, v.B8 + j0 * L.planeB, L.planeB, L, 0, SP, c.st);
+}
+
+// phase 2: residue planes j0..j1-1 (one launch; conv_32i_2_8u fused into the epilogue)
+static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1, hipStream_t st) {
+    const Layout &L = v.L;
+    gemm_i8(v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB, L, j1 - j0, Epi::RESIDUE, v.R + j0 * L.planeR, nullptr,
+            nullptr, sub_mod_params(N, j0, j1), st);
+}
+
+// phase 3: CRT + scaling + BLAS epilogue over all N residue planes
+static void phase_crt(const Views &v, unsigned N, OutType ot, const void *alpha, const void *beta, void *C, size_t ldc,
+                      hipStream_t st) {
+    const CrtParams CP = make_crt_params(N, ot == OutType::F32 || ot == OutType::C32);
+    crt_inverse(v.R, v.L, v.sftA, v.sftB, CP, ot, alpha, beta, C, ldc, st);
+}
+
+static int run(const Call &c, double *phase_ns) {
+    const Views v = views(c.work, c.m, c.n, c.k, c.N, c.cplx);
 
     const bool want_events = phase_ns != nullptr;
     bool record;
@@ -99,32 +173,16 @@ static int run(const Call &c, double *phase_ns) {
     }
     if (record) (void)hipEventRecord(rec.start, c.st);
 
-    if (c.fast) {
-        const float log2M = oz2_log2M_fast[c.N - 2];
-        split_stats(c.A, c.k, c.m, c.VT, false, log2M, sftA, c.st);
-        split_stats(c.B, c.k, c.n, c.VT, false, log2M, sftB, c.st);
-    } else {
-        const float log2M = oz2_log2M_accu[c.N - 2];
-        split_stats(c.A, c.k, c.m, c.VT, true, 0.f, sft0, c.st);
-        split_stats(c.B, c.k, c.n, c.VT, true, 0.f, sft0 + L.m_pad, c.st);
-        split_encode(c.A, true, c.m, c.k, sft0, A8, L.planeA, L, 1, MP, c.st);
-        split_encode(c.B, false, c.n, c.k, sft0 + L.m_pad, B8, L.planeB, L, 1, MP, c.st);
-        (void)hipMemsetAsync(bound, 0, (L.m_pad + L.n_pad) * sizeof(int32_t), c.st);
-        gemm_i8(A8, B8, L, 1, Epi::BOUND, nullptr, bound, bound + L.m_pad, MP, c.st);
-        split_finalize_accurate(sft0, bound, c.m, log2M, sftA, c.st);
-        split_finalize_accurate(sft0 + L.m_pad, bound + L.m_pad, c.n, log2M, sftB, c.st);
-    }
-    split_encode(c.A, true, c.m, c.k, sftA, A8, L.planeA, L, 0, MP, c.st);
-    split_encode(c.B, false, c.n, c.k, sftB, B8, L.planeB, L, 0, MP, c.st);
+    phase_split(c, v, 0, c.N, false);
     if (record) (void)hipEventRecord(rec.ev[0], c.st);
 
-    gemm_i8(A8, B8, L, c.N, Epi::RESIDUE, R, nullptr, nullptr, MP, c.st);
+    phase_products(v, c.N, 0, c.N, c.st);
     if (record) {
         (void)hipEventRecord(rec.ev[1], c.st);
         (void)hipEventRecord(rec.ev[2], c.st);
     }
 
-    crt_inverse(R, L, sftA, sftB, CP, c.ot, c.alpha, c.beta, c.C, c.ldc, c.st);
+    phase_crt(v, c.N, c.ot, c.alpha, c.beta, c.C, c.ldc, c.st);
     if (record) (void)hipEventRecord(rec.ev[3], c.st);
     if (!launch_ok()) return GEMMUL8_E_HIP;
 
@@ -206,6 +264,63 @@ int gemmul8_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k,
     if (rc != GEMMUL8_OK) return rc;
     if (m == 0 || n == 0) return GEMMUL8_OK;
     return oz2::run(c, phase_ns);
+}
+
+int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
+                        void *work, int compute_type) {
+    oz2::Call c{};
+    const int rc = oz2::prepare(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, nullptr, A, lda, B, ldb, nullptr,
+                                nullptr, m, num_moduli, 0, work, compute_type, c);
+    if (rc != GEMMUL8_OK) return rc;
+    if (m == 0 && n == 0) return GEMMUL8_OK;
+    const oz2::Views v = oz2::views(work, m, n, k, num_moduli, c.cplx);
+    if (m == 0 || n == 0) {  // an empty block contributes nothing to the other operand's maxima
+        (void)hipMemsetAsync(v.bound, 0, (v.L.m_pad + v.L.n_pad) * sizeof(int32_t), c.st);
+        return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+    }
+    oz2::phase_bound(c, v);
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b, int type_c,
+                  const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli, int fastmode, void *work,
+                  int compute_type, unsigned mod_begin, unsigned mod_end, int flags) {
+    oz2::Call c{};
+    const int rc = oz2::prepare(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, nullptr, A, lda, B, ldb, nullptr,
+                                nullptr, m, num_moduli, fastmode, work, compute_type, c);
+    if (rc != GEMMUL8_OK) return rc;
+    if (mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::phase_split(c, oz2::views(work, m, n, k, num_moduli, c.cplx), mod_begin, mod_end,
+                     (flags & GEMMUL8_SPLIT_BOUND_READY) != 0);
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, void *work,
+                     unsigned mod_begin, unsigned mod_end) {
+    if (num_moduli < 2 || num_moduli > 20 || mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
+    if (compute_type != GEMMUL8_REAL_DEFAULT && compute_type != GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE)
+        return GEMMUL8_E_UNSUPPORTED;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    const oz2::Views v = oz2::views(work, m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
+    oz2::phase_products(v, num_moduli, mod_begin, mod_end, static_cast<hipStream_t>(stream));
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_recombine(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c, int compute_type,
+                      const void *alpha, const void *beta, void *C, size_t ldc, void *work) {
+    if (num_moduli < 2 || num_moduli > 20) return GEMMUL8_E_MODULI;
+    if (type_c < 0 || type_c > 3) return GEMMUL8_E_TYPES;
+    const bool cp = compute_type != GEMMUL8_REAL_DEFAULT;
+    if (cp != oz2::dt_cplx(type_c)) return GEMMUL8_E_TYPES;
+    if (cp && compute_type != GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE) return GEMMUL8_E_UNSUPPORTED;
+    if (ldc < m) return GEMMUL8_E_SIZE;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    const oz2::Views v = oz2::views(work, m, n, k, num_moduli, cp);
+    oz2::phase_crt(v, num_moduli, static_cast<oz2::OutType>(type_c), alpha, beta, C, ldc,
+                   static_cast<hipStream_t>(stream));
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
 
 void gemmul8_timing_enable(int on) {

@@ -40,6 +40,10 @@ def _load():
     lib.gemmul8_work_size.argtypes = [sz, sz, sz, u, i]
     lib.gemmul8_gemm.restype = i
     lib.gemmul8_gemm.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, p, sz, p, sz, p, p, sz, u, i, p, i, d]
+    lib.gemmul8_split.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, sz, p, sz, u, i, p, i, u, u, i]
+    lib.gemmul8_split_bound.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, sz, p, sz, u, p, i]
+    lib.gemmul8_products.argtypes = [p, sz, sz, sz, u, i, p, u, u]
+    lib.gemmul8_recombine.argtypes = [p, sz, sz, sz, u, i, i, p, p, p, sz, p]
     lib.gemmul8_timing_enable.argtypes = [i]
     lib.gemmul8_timing_read.argtypes = [d, ctypes.POINTER(ctypes.c_int)]
     lib.gemmul8_layout.argtypes = [sz, sz, sz, u, i, ctypes.POINTER(ctypes.c_size_t)]
@@ -100,6 +104,54 @@ def gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fas
                           work.data_ptr(), computeType, pt)
     _check(rc)
     return list(pt) if phase_times else None
+
+
+# ---- phase entry points (gemm == split + products + recombine; used by gemmul8.dist) ----
+SPLIT_BOUND_READY = 1
+
+
+def split(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, work, out_dtype, mod_begin=0, mod_end=None,
+          computeType=REAL_DEFAULT, stream=None, bound_ready=False):
+    """Shifts of op(A)/op(B) and the int8 slices of moduli [mod_begin, mod_end) into `work`."""
+    mod_end = num_moduli if mod_end is None else mod_end
+    _check(lib.gemmul8_split(_stream(stream), opA, opB, m, n, k, _DTYPE[A.dtype], _DTYPE[B.dtype], _DTYPE[out_dtype],
+                             A.data_ptr(), lda, B.data_ptr(), ldb, num_moduli, int(bool(fastmode)), work.data_ptr(),
+                             computeType, mod_begin, mod_end, SPLIT_BOUND_READY if bound_ready else 0))
+
+
+def split_bound(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, work, out_dtype, computeType=REAL_DEFAULT,
+                stream=None):
+    """Accurate mode: bound product maxima into `work`; returns (rowmax [m], colmax [n]) int32 views."""
+    _check(lib.gemmul8_split_bound(_stream(stream), opA, opB, m, n, k, _DTYPE[A.dtype], _DTYPE[B.dtype],
+                                   _DTYPE[out_dtype], A.data_ptr(), lda, B.data_ptr(), ldb, num_moduli,
+                                   work.data_ptr(), computeType))
+    L = layout(m, n, k, num_moduli, computeType)
+    o = L["offBound"]
+    rowmax = work[o:o + 4 * m].view(torch.int32)
+    colmax = work[o + 4 * L["m_pad"]:o + 4 * L["m_pad"] + 4 * n].view(torch.int32)
+    return rowmax, colmax
+
+
+def products(m, n, k, num_moduli, work, mod_begin=0, mod_end=None, computeType=REAL_DEFAULT, stream=None):
+    """Residue planes of moduli [mod_begin, mod_end) (one MFMA launch) into `work`."""
+    mod_end = num_moduli if mod_end is None else mod_end
+    _check(lib.gemmul8_products(_stream(stream), m, n, k, num_moduli, computeType, work.data_ptr(), mod_begin,
+                                mod_end))
+
+
+def recombine(m, n, k, num_moduli, alpha, beta, C, ldc, work, computeType=REAL_DEFAULT, stream=None):
+    """CRT of all residue planes in `work` + scaling + alpha/beta epilogue into C."""
+    al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
+    _check(lib.gemmul8_recombine(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], computeType, al.ctypes.data,
+                                 be.ctypes.data, C.data_ptr(), ldc, work.data_ptr()))
+
+
+def residue_planes(work, m, n, k, num_moduli, mod_begin=0, mod_end=None, computeType=REAL_DEFAULT):
+    """uint8 view [mod_end - mod_begin, planeR] of the residue planes inside `work` (no copy)."""
+    mod_end = num_moduli if mod_end is None else mod_end
+    L = layout(m, n, k, num_moduli, computeType)
+    start = L["offR"] + mod_begin * L["planeR"]
+    return work[start:start + (mod_end - mod_begin) * L["planeR"]].view(mod_end - mod_begin, L["planeR"])
 
 
 def alloc_work(m, n, k, num_moduli, computeType=REAL_DEFAULT, device="cuda"):

@@ -28,6 +28,7 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         p, sz, u, i, c = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int, ctypes.c_char
         _lib.oz2o_scaling.argtypes = [c, c, i, i, sz, sz, sz, p, sz, p, sz, u, i, i, p, p, p, p]
+        _lib.oz2o_scaling_ex.argtypes = [c, c, i, i, sz, sz, sz, p, sz, p, sz, u, i, i, p, p, p, p, p, p]
         _lib.oz2o_residues.argtypes = [sz, sz, sz, u, p, p, p]
         _lib.oz2o_crt.argtypes = [c, i, sz, sz, u, p, p, p, p, p, p, sz, i]
         _lib.oz2o_gemm.argtypes = [c, c, c, i, i, sz, sz, sz, p, p, sz, p, sz, p, p, sz, u, i, i, i, p, p]
@@ -47,8 +48,11 @@ def default_vt(ta, tb):
     return 512 if (ta == np.float32 and tb == np.float32) else 128
 
 
-def scaling(A, B, num_moduli, fastmode=True, opA=0, opB=0, vt=None):
-    """Returns (A8 [N, mr, kr], B8 [N, n, kr], sftA [m], sftB [n]) for column-major A, B."""
+def scaling(A, B, num_moduli, fastmode=True, opA=0, opB=0, vt=None, colmax_in=None, want_colmax=False):
+    """Returns (A8 [N, mr, kr], B8 [N, n, kr], sftA [m], sftB [n]) for column-major A, B.
+
+    Accurate mode only: colmax_in replaces the bound product's column maxima (row-block
+    sharding); want_colmax appends this call's column maxima to the result."""
     A = np.asfortranarray(A)
     B = np.asfortranarray(B)
     m = A.shape[1] if opA else A.shape[0]
@@ -61,11 +65,14 @@ def scaling(A, B, num_moduli, fastmode=True, opA=0, opB=0, vt=None):
     B8 = np.zeros((num_moduli, n, kr), np.int8)
     sA = np.zeros(m, np.int16)
     sB = np.zeros(n, np.int16)
-    rc = lib().oz2o_scaling(tcode(A.dtype), tcode(B.dtype), opA, opB, m, n, k, _ptr(A), A.shape[0], _ptr(B),
-                            B.shape[0], num_moduli, int(fastmode), vt, _ptr(A8), _ptr(B8), _ptr(sA), _ptr(sB))
+    cin = None if colmax_in is None else np.ascontiguousarray(colmax_in, np.int32)
+    cout = np.zeros(n, np.int32) if want_colmax else None
+    rc = lib().oz2o_scaling_ex(tcode(A.dtype), tcode(B.dtype), opA, opB, m, n, k, _ptr(A), A.shape[0], _ptr(B),
+                               B.shape[0], num_moduli, int(fastmode), vt, _ptr(A8), _ptr(B8), _ptr(sA), _ptr(sB),
+                               None if cin is None else _ptr(cin), None if cout is None else _ptr(cout))
     if rc:
         raise ValueError(f"oz2o_scaling rc={rc}")
-    return A8, B8, sA, sB
+    return (A8, B8, sA, sB, cout) if want_colmax else (A8, B8, sA, sB)
 
 
 def residues(A8, B8):

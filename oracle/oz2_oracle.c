@@ -367,9 +367,12 @@ static void accurate_vectors(const vec_src *s, size_t nvec, size_t k, unsigned N
 /* opA/opB: 0 = N, 1 = T.  VT: threads_scaling of the reference entry point
  * (gemmul8.cu:206-222 etc.: 128 for gemm<double>, mixed and complex, 512 for
  * gemm<float>).  Returns 0 on success. */
-int oz2o_scaling(char ta, char tb, int opA, int opB, size_t m, size_t n, size_t k, const void *A, size_t lda,
-                 const void *B, size_t ldb, unsigned N, int fastmode, int VT, int8_t *A8, int8_t *B8,
-                 int16_t *sftA, int16_t *sftB) {
+/* colmax_out (optional): the bound product's column maxima of this call (accurate mode);
+ * colmax_in (optional): column maxima to use instead (a row-block shard after the MAX
+ * all-reduce over the other blocks, gemmul8/dist.py). */
+int oz2o_scaling_ex(char ta, char tb, int opA, int opB, size_t m, size_t n, size_t k, const void *A, size_t lda,
+                    const void *B, size_t ldb, unsigned N, int fastmode, int VT, int8_t *A8, int8_t *B8,
+                    int16_t *sftA, int16_t *sftB, const int32_t *colmax_in, int32_t *colmax_out) {
     if (N < 2 || N > 20) return -1;
     int cp = is_cplx(ta) || is_cplx(tb);
     if (cp && (!is_cplx(ta) || !is_cplx(tb))) return -2;
@@ -413,11 +416,19 @@ int oz2o_scaling(char ta, char tb, int opA, int opB, size_t m, size_t n, size_t 
         }
         amB[c] = mx;
     }
+    if (colmax_out) memcpy(colmax_out, amB, n * sizeof(int32_t));
+    if (colmax_in) memcpy(amB, colmax_in, n * sizeof(int32_t));
     float log2M = oz2_log2M_accu[N - 2];
     accurate_vectors(&sa, m, k, N, amA, s0A, log2M, A8, kr, sftA);
     accurate_vectors(&sb, n, k, N, amB, s0B, log2M, B8, kr, sftB);
     free(A6); free(B6); free(s0A); free(s0B); free(amA); free(amB);
     return 0;
+}
+
+int oz2o_scaling(char ta, char tb, int opA, int opB, size_t m, size_t n, size_t k, const void *A, size_t lda,
+                 const void *B, size_t ldb, unsigned N, int fastmode, int VT, int8_t *A8, int8_t *B8,
+                 int16_t *sftA, int16_t *sftB) {
+    return oz2o_scaling_ex(ta, tb, opA, opB, m, n, k, A, lda, B, ldb, N, fastmode, VT, A8, B8, sftA, sftB, NULL, NULL);
 }
 
 /* conv_32i_2_8u (conv_32i_2_8u.hpp:7-56) */

@@ -1,0 +1,131 @@
+"""Multi-process tests of gemmul8.dist on the CPU with the gloo backend.
+
+The communication pattern (row blocks gathered on the root; moduli sharded with residue
+planes sent to the root) runs for real across 2 and 3 processes; the compute steps are the
+CPU oracle (test infrastructure) injected through the ``ops`` hook, so the result must be
+bit-identical to one oracle call on the whole problem.  The GPU variant (HipOps over RCCL)
+is covered in test_gpu_phases.py."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+class OracleOps:
+    """CPU stand-in for gemmul8.dist.HipOps (tests only)."""
+
+    def __init__(self):
+        from oracle import oracle as O
+        self.O = O
+
+    def full(self, A, B, N, fast, out_dtype):
+        npt = torch.empty((), dtype=out_dtype).numpy().dtype
+        C = self.O.gemm(A.numpy(), B.numpy(), N, fast, out_dtype=npt)
+        return torch.from_numpy(np.ascontiguousarray(C))
+
+    def row_bound(self, A, B, N, out_dtype):
+        *_, colmax = self.O.scaling(A.numpy(), B.numpy(), N, False, want_colmax=True)
+        colmax = torch.from_numpy(colmax)
+        return colmax, {"A": A, "B": B, "N": N, "colmax": colmax, "dtype": out_dtype}
+
+    def finish_rows(self, st):
+        A8, B8, sA, sB = self.O.scaling(st["A"].numpy(), st["B"].numpy(), st["N"], False,
+                                        colmax_in=st["colmax"].numpy())
+        npt = torch.empty((), dtype=st["dtype"]).numpy().dtype
+        C = self.O.crt(self.O.residues(A8, B8), sA, sB, npt)
+        return torch.from_numpy(np.ascontiguousarray(C))
+
+    def partial(self, A, B, N, fast, out_dtype, j0, j1, need_shifts):
+        A8, B8, sA, sB = self.O.scaling(A.numpy(), B.numpy(), N, fast)
+        full = self.O.residues(A8, B8)
+        R = np.zeros_like(full)  # only this rank's planes; the root must receive the rest
+        R[j0:j1] = full[j0:j1]
+        Rt = torch.from_numpy(R).reshape(N, -1)
+        npt = torch.empty((), dtype=out_dtype).numpy().dtype
+        return Rt[j0:j1], {"R": Rt, "shape": full.shape, "sA": sA, "sB": sB, "dtype": npt}
+
+    def all_planes(self, st):
+        return st["R"]
+
+    def sync(self):
+        pass
+
+    def finish(self, st):
+        C = self.O.crt(st["R"].numpy().reshape(st["shape"]), st["sA"], st["sB"], st["dtype"])
+        return torch.from_numpy(np.ascontiguousarray(C))
+
+
+def _worker(rank, world, port, case, outdir):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "mixed-gemmul8_amd")]
+    from gemmul8 import dist as GD
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m, n, k, N, fast, dt = case
+        rng = np.random.default_rng(7)
+        A = ((rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))).astype(dt)
+        B = ((rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))).astype(dt)
+        ops = OracleOps()
+        Cm = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, ops=ops)
+        r0, r1 = GD.row_partition(m, world, align=16)[rank]
+        Cr = GD.matmul_rows(torch.from_numpy(A[r0:r1].copy()), torch.from_numpy(B), N, fast, gather=True, ops=ops)
+        if rank == 0:
+            np.save(os.path.join(outdir, "moduli.npy"), Cm.numpy())
+            np.save(os.path.join(outdir, "rows.npy"), Cr.numpy())
+        else:
+            assert Cm is None and Cr is None
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,case", [
+    (2, (70, 50, 90, 14, True, np.float64)),
+    (2, (64, 33, 120, 5, False, np.float64)),
+    (3, (100, 40, 64, 14, True, np.float64)),
+    (3, (48, 30, 50, 8, True, np.float32)),
+    (3, (90, 30, 70, 9, False, np.float64)),
+])
+def test_sharded_equals_single_call(tmp_path, world, case):
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
+    m, n, k, N, fast, dt = case
+    rng = np.random.default_rng(7)
+    A = ((rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))).astype(dt)
+    B = ((rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))).astype(dt)
+    C = O.gemm(A, B, N, fast)
+    for name in ("moduli", "rows"):
+        got = np.load(tmp_path / f"{name}.npy")
+        assert got.shape == C.shape
+        assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C).view(np.uint8)), name
+
+
+def test_partitions():
+    sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd"))
+    from gemmul8.dist import moduli_partition, row_partition
+    assert moduli_partition(14, 8) == [(0, 2), (2, 4), (4, 6), (6, 8), (8, 10), (10, 12), (12, 13), (13, 14)]
+    assert moduli_partition(3, 4) == [(0, 1), (1, 2), (2, 3), (3, 3)]
+    for N in range(2, 21):
+        for w in (1, 2, 3, 8):
+            p = moduli_partition(N, w)
+            assert p[0][0] == 0 and p[-1][1] == N and all(a[1] == b[0] for a, b in zip(p, p[1:]))
+            assert max(b - a for a, b in p) - min(b - a for a, b in p) <= 1
+    assert row_partition(16384, 8) == [(2048 * r, 2048 * (r + 1)) for r in range(8)]
+    rp = row_partition(1000, 3)
+    assert rp == [(0, 512), (512, 768), (768, 1000)]
+    assert row_partition(100, 4)[-1] == (100, 100)

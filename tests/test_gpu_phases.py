@@ -1,0 +1,138 @@
+"""GPU: the phase entry points (gemmul8_split / _split_bound / _products / _recombine) and the
+multi-GPU partitions of gemmul8.dist, run through the native library.
+
+Every composition must reproduce the single gemmul8_gemm call (itself bit-exact against the
+oracle, test_gpu_parity.py) bit for bit:
+  * moduli computed in separate ranges (the modulus-sharded layout),
+  * accurate-mode row blocks whose bound-product column maxima are MAX-combined,
+  * gemmul8.dist.matmul_rows / matmul_moduli in a one-rank RCCL group.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(m, n, seed, dtype):
+    import torch
+    g = torch.Generator().manual_seed(seed)
+    x = (torch.rand((m, n), generator=g, dtype=torch.float64) - 0.5) * torch.exp(
+        torch.randn((m, n), generator=g, dtype=torch.float64))
+    return x.to(dtype).cuda()
+
+
+def _single(A, B, N, fast, out_dtype):
+    import torch
+    import gemmul8 as G
+    m, k = A.shape
+    n = B.shape[1]
+    Ct = torch.empty((n, m), dtype=out_dtype, device="cuda")
+    work = G.alloc_work(m, n, k, N)
+    G.gemm(G.OP_T, G.OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, N, fast, work)
+    torch.cuda.synchronize()
+    return Ct.t().contiguous()
+
+
+def _same(a, b):
+    import torch
+    return a.shape == b.shape and torch.equal(a.contiguous().view(torch.uint8), b.contiguous().view(torch.uint8))
+
+
+@pytest.mark.parametrize("m,n,k,N,fast,dt", [
+    (300, 260, 500, 14, True, "f64"),
+    (257, 190, 333, 9, False, "f64"),
+    (200, 128, 256, 6, True, "f32"),
+])
+def test_moduli_ranges_compose(m, n, k, N, fast, dt):
+    import torch
+    import gemmul8 as G
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    A, B = _rand(m, k, 1, tdt), _rand(k, n, 2, tdt)
+    ref = _single(A, B, N, fast, tdt)
+    work = G.alloc_work(m, n, k, N)
+    for j0, j1 in ((0, 1), (1, N // 2), (N // 2, N)):
+        G.split(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, fast, work, tdt, j0, j1)
+        G.products(m, n, k, N, work, j0, j1)
+    Ct = torch.empty((n, m), dtype=tdt, device="cuda")
+    G.recombine(m, n, k, N, 1.0, 0.0, Ct, m, work)
+    torch.cuda.synchronize()
+    assert _same(Ct.t(), ref)
+
+
+def test_accurate_row_blocks_with_combined_bound():
+    import torch
+    from gemmul8 import dist as GD
+    m, n, k, N = 700, 300, 400, 12
+    A, B = _rand(m, k, 3, torch.float64), _rand(k, n, 4, torch.float64)
+    ref = _single(A, B, N, False, torch.float64)
+    ops = GD.HipOps()
+    blocks = GD.row_partition(m, 3)
+    states, colmaxes = [], []
+    for r0, r1 in blocks:
+        cm, st = ops.row_bound(A[r0:r1].contiguous(), B, N, torch.float64)
+        colmaxes.append(cm)
+        states.append(st)
+    torch.cuda.synchronize()
+    comb = torch.stack([c.clone() for c in colmaxes]).amax(0)
+    for c in colmaxes:  # what the MAX all-reduce leaves in every rank's workspace
+        c.copy_(comb)
+    out = torch.cat([ops.finish_rows(st) for st in states], 0)
+    torch.cuda.synchronize()
+    assert _same(out, ref)
+    # without the exchange the column shifts differ (the reason the all-reduce exists)
+    cm, st = ops.row_bound(A[:256].contiguous(), B, N, torch.float64)
+    alone = ops.finish_rows(st)
+    torch.cuda.synchronize()
+    assert not _same(alone, ref[:256])
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_dist_one_rank_rccl():
+    import torch
+    import torch.distributed as dist
+    from gemmul8 import dist as GD
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        m, n, k, N = 520, 300, 260, 14
+        A, B = _rand(m, k, 5, torch.float64), _rand(k, n, 6, torch.float64)
+        ref = _single(A, B, N, True, torch.float64)
+        assert _same(GD.matmul_moduli(A, B, N, True), ref)
+        assert _same(GD.matmul_rows(A, B, N, True, gather=True), ref)
+        refa = _single(A, B, N, False, torch.float64)
+        assert _same(GD.matmul_rows(A, B, N, False), refa)
+        assert _same(GD.matmul_moduli(A, B, N, False), refa)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_moduli_shards_assembled_on_root():
+    """The modulus-sharded data flow of matmul_moduli with 4 simulated ranks in one process:
+    each 'rank' fills its own workspace, the root copies the planes in (the P2P receive)."""
+    import torch
+    from gemmul8 import dist as GD
+    m, n, k, N = 384, 256, 300, 14
+    A, B = _rand(m, k, 7, torch.float64), _rand(k, n, 8, torch.float64)
+    ref = _single(A, B, N, True, torch.float64)
+    ops = GD.HipOps()
+    parts = GD.moduli_partition(N, 4)
+    shards = [ops.partial(A, B, N, True, torch.float64, a, b, r == 0) for r, (a, b) in enumerate(parts)]
+    root_st = shards[0][1]
+    allp = ops.all_planes(root_st)
+    for r, (a, b) in enumerate(parts):
+        if r:
+            allp[a:b].copy_(shards[r][0])
+    out = ops.finish(root_st)
+    torch.cuda.synchronize()
+    assert _same(out, ref)
