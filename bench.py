@@ -9,11 +9,15 @@ A and B identical as in GEMMul8/testing/test_double.cu:273-274).
 One "step" = one gemmul8 DGEMM call (scaling -> N int8 products -> CRT) with the
 operands resident in HBM.  TFLOP/s = 2*m*n*k / time (test_double.cu:440).
 
-Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling by output row
-blocks -- rank r computes the 8192-row block r of C = A * B for an
-(8192*N) x 8192 x 8192 product; B is replicated, no data-path collective
-(the shifts of a row depend only on that row, so the blocks are bit-identical
-to a single-GPU run of the whole product).
+Multi-GPU (torchrun, one process per GPU, RCCL), --partition:
+  rows (default)  weak scaling by output row blocks -- rank r computes the 8192-row
+                  block r of C = A * B for an (8192*N) x 8192 x 8192 product; B is
+                  replicated, no data-path collective (fast-mode shifts of a row depend
+                  only on that row, so the blocks are bit-identical to a single-GPU run
+                  of the whole product; gemmul8/dist.py).
+  moduli          strong scaling of ONE m=n=k=size product: rank r computes the residue
+                  planes of its moduli and sends them to rank 0 (P2P over xGMI), which
+                  runs the CRT (gemmul8.dist.matmul_moduli).
 
 Prints ONE JSON line on rank 0.
 """
@@ -42,6 +46,7 @@ def parse():
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--moduli", type=int, default=14)
     ap.add_argument("--accurate", action="store_true")
+    ap.add_argument("--partition", choices=["rows", "moduli"], default="rows")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--no-dgemm", action="store_true")
@@ -113,16 +118,36 @@ def main():
     m = n = k = args.size
     N = args.moduli
     dev = torch.device("cuda", torch.cuda.current_device())
-    stream = torch.cuda.current_stream()
-    # inputs (column-major; the (k, m) row-major tensor holds the column-major m x k matrix)
-    seed = 123456 + rank
-    A = G.randmat(m, k, torch.float64, 0.5, seed, dev)
-    B = G.randmat(k, n, torch.float64, 0.5, 123456, dev)
-    C = torch.empty((n, m), dtype=torch.float64, device=dev)
-    work = G.alloc_work(m, n, k, N, G.REAL_DEFAULT, dev)
+    if args.partition == "moduli" and world > 1:
+        from gemmul8 import dist as GD
+        # row-major m x k / k x n operands (randmat(k, m) is the column-major k x m matrix)
+        Arm = G.randmat(k, m, torch.float64, 0.5, 123456, dev)
+        Brm = G.randmat(n, k, torch.float64, 0.5, 654321, dev)
+        A = B = None
 
-    def step():
-        G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, not args.accurate, work)
+        def step():
+            GD.matmul_moduli(Arm, Brm, N, not args.accurate)
+    else:
+        # inputs (column-major; the (k, m) row-major tensor holds the column-major m x k matrix)
+        seed = 123456 + rank
+        A = G.randmat(m, k, torch.float64, 0.5, seed, dev)
+        B = G.randmat(k, n, torch.float64, 0.5, 123456, dev)
+        C = torch.empty((n, m), dtype=torch.float64, device=dev)
+        work = G.alloc_work(m, n, k, N, G.REAL_DEFAULT, dev)
+
+        def step():
+            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, not args.accurate, work)
+
+        if args.accurate and world > 1:
+            # accurate mode couples B's column shifts to every row block: one MAX all-reduce of
+            # the bound product's column maxima per call (gemmul8.dist.matmul_rows)
+            from gemmul8 import dist as GD
+            Arm = G.randmat(k, m, torch.float64, 0.5, seed, dev)
+            Brm = G.randmat(n, k, torch.float64, 0.5, 123456, dev)
+            A = B = None
+
+            def step():
+                GD.matmul_rows(Arm, Brm, N, False)
 
     for _ in range(args.warmup):
         step()
@@ -139,14 +164,20 @@ def main():
     dt = max_over_ranks(dt, world)
     ms_per_step = dt / args.steps * 1e3
     flops = 2.0 * m * n * k
-    value = flops * world * args.steps / dt / 1e12
+    strong = args.partition == "moduli" and world > 1
+    value = flops * (1 if strong else world) * args.steps / dt / 1e12
 
     out = None
     if rank == 0:
         avg = [x / max(calls, 1) for x in phase_ms]
         # dominant kernel: the int8 products (one launch per call, all moduli)
         gemm_ms = avg[1]
-        ops = 2.0 * m * n * k * N
+        planes = N
+        if strong:
+            from gemmul8 import dist as GD
+            a, b = GD.moduli_partition(N, world)[0]
+            planes = b - a  # rank 0's share of the moduli
+        ops = 2.0 * m * n * k * planes
         achieved = ops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(INT8_PEAK_TOPS, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4), "traffic": traffic_from_profile(),
@@ -154,7 +185,7 @@ def main():
                     "avg_launch_ms": round(gemm_ms, 4)}
         extra = {"phase_ms": {"scaling": round(avg[0], 4), "int8_products": round(avg[1], 4),
                               "inverse_scaling": round(avg[3], 4)}}
-        if not args.no_accuracy:
+        if not args.no_accuracy and A is not None:
             # accuracy against a double-double reference (testing/eval.hpp semantics)
             step()
             torch.cuda.synchronize()
@@ -163,7 +194,7 @@ def main():
             extra["relerr_max"] = emax
             extra["relerr_median"] = emed
             del C1, C2
-        if not args.no_dgemm:
+        if not args.no_dgemm and A is not None:
             Ar = A.t()  # logical m x k view
             Br = B.t()
             for _ in range(2):
@@ -187,7 +218,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": round(value / world / GH200_PUBLISHED_TFLOPS, 3),
             "vs_baseline_ref": "GH200 published OS2-fast-14 8192 (72.13 TFLOP/s, BASELINE.md); per-GPU ratio",
             "dtype": "i8",
@@ -198,7 +229,7 @@ def main():
                        if (m == 8192 and N == 14 and not args.accurate) else
                        f"DGEMM emulation m=n=k={m}, num_moduli={N}, {'accurate' if args.accurate else 'fast'} mode",
                        "m": m, "n": n, "k": k, "num_moduli": N, "fastmode": not args.accurate,
-                       "parallelism": f"row-block x{world}" if world > 1 else "single"},
+                       "parallelism": (f"{args.partition} x{world}" if world > 1 else "single")},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -304,7 +304,27 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
         return GEMMUL8_E_UNSUPPORTED;
     if (m == 0 || n == 0) return GEMMUL8_OK;
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
-    oz2::phase_products(v, num_moduli, mod_begin, mod_end, static_cast<hipStream_t>(stream));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // with timing enabled the launch is bracketed like gemmul8_gemm's product phase (phases 0/3 read 0)
+    bool record;
+    oz2::timing::Rec rec{};
+    {
+        std::lock_guard<std::mutex> g(oz2::timing::mu);
+        record = oz2::timing::enabled;
+        if (record) rec = oz2::timing::acquire();
+    }
+    if (record) {
+        (void)hipEventRecord(rec.start, st);
+        (void)hipEventRecord(rec.ev[0], st);
+    }
+    oz2::phase_products(v, num_moduli, mod_begin, mod_end, st);
+    if (record) {
+        (void)hipEventRecord(rec.ev[1], st);
+        (void)hipEventRecord(rec.ev[2], st);
+        (void)hipEventRecord(rec.ev[3], st);
+        std::lock_guard<std::mutex> g(oz2::timing::mu);
+        oz2::timing::pending.push_back(rec);
+    }
     return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
 

@@ -157,6 +157,27 @@ def test_alpha_beta(alpha, beta):
     check_full(A.astype(np.float32), B.astype(np.float32), 8, alpha=alpha, beta=beta, C0=C0.astype(np.float32))
 
 
+TYPE_COMBOS = [  # the 12 reference specializations (gemmul8.hpp:49-287)
+    ("d", "d", "d"), ("s", "s", "s"), ("d", "s", "d"), ("s", "d", "d"), ("d", "s", "s"), ("s", "d", "s"),
+    ("c", "c", "c"), ("z", "z", "z"), ("z", "c", "z"), ("c", "z", "z"), ("z", "c", "c"), ("c", "z", "c"),
+]
+_NPT = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}
+
+
+@pytest.mark.parametrize("ta,tb,tc", TYPE_COMBOS)
+def test_every_specialization(ta, tb, tc):
+    rng = np.random.default_rng(len(ta + tb + tc) + ord(ta) * 7 + ord(tb) * 3 + ord(tc))
+    A = randmat_np(rng, 70, 90, dtype=_NPT[ta])
+    B = randmat_np(rng, 90, 50, dtype=_NPT[tb])
+    check_full(A, B, 9, out_dtype=_NPT[tc])
+
+
+@pytest.mark.parametrize("m,n,k,N", [(64, 40, 5000, 14), (513, 3, 70, 8), (3, 600, 129, 20), (256, 256, 64, 2)])
+def test_extreme_shapes(m, n, k, N):
+    rng = np.random.default_rng(m + n + k)
+    check_full(randmat_np(rng, m, k), randmat_np(rng, k, n), N)
+
+
 def test_zero_rows_and_cols():
     rng = np.random.default_rng(5)
     A, B = randmat_np(rng, 50, 60), randmat_np(rng, 60, 40)

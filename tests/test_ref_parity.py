@@ -40,7 +40,10 @@ CODES = {"d": 0, "s": 1, "z": 2, "c": 3}
     ("d", "s", "d", 2048, 1536, 1000, 10, 0),
     ("d", "d", "d", 1536, 1024, 2048, 14, 0),
     ("z", "z", "z", 512, 640, 384, 12, 1),
-    ("d", "d", "d", 8192, 8192, 8192, 14, 1),
+    ("d", "d", "d", 8192, 8192, 8192, 14, 1),   # cfg2
+    ("s", "s", "s", 1024, 1024, 1024, 4, 1),     # cfg1 shape on the GPU
+    ("d", "s", "d", 8192, 8192, 8192, 10, 0),    # cfg4
+    ("z", "z", "z", 4096, 4096, 4096, 12, 1),    # cfg5
 ])
 def test_same_inputs_same_bits(case):
     import torch
