@@ -8,16 +8,21 @@
 // modulus).  The accurate-mode bound product (scaling.hpp:3113-3121) runs the same
 // main loop with a row/column-max epilogue instead of an m x n int32 buffer.
 //
-// Block: 256 threads = 4 waves (one per SIMD) as 2 (M) x 2 (N); each wave owns a
-// 128 x 128 sub-tile = 4 x 4 fragments of 32x32 (256 accumulator registers).
-// Pipeline per 64-deep k-step:
-//   * operand panels (16 KiB each, pre-arranged in fragment order by split.hip)
-//     stream HBM -> LDS through a 4-slot ring (128 KiB) with global_load_lds issued
-//     three k-steps ahead (inline asm, one DMA per 4 MFMAs, waits counted by hand);
-//     measured on MI355X: 3 slots 1.87 ms, 4 slots 1.63 ms, 5 slots 1.63 ms (N=4, 8192^3);
-//   * one barrier per k-step;
-//   * the next k-step's 16 fragment reads (ds_read_b128, conflict-free 1 KiB sweeps)
-//     are issued between the current k-step's 32 MFMAs (register double buffer).
+// Block: 512 threads = 8 waves, two per SIMD, as 2 (M) x 4 (N); each wave owns a
+// 128 x 64 sub-tile = 4 x 2 fragments of 32x32 (128 accumulator registers).
+// The two waves of a SIMD PING-PONG: waves 0-3 (group 0) and 4-7 (group 1) run the
+// same per-k-step sequence
+//     load interval:  12 fragment reads (ds_read_b128, 1 KiB conflict-free sweeps)
+//                     + 4 LDS-DMA pieces of the step D ahead; wait for them
+//     barrier
+//     MFMA interval:  16 MFMAs
+//     barrier
+// with group 1 one barrier behind, so on every SIMD one wave's MFMAs run while the
+// other wave issues its LDS reads and LDS-DMA (whose issue costs 60-185 cycles each
+// and, with one wave per SIMD, stalled the matrix core).
+// Operand panels (16 KiB, pre-arranged in fragment order by split.hip) stream
+// HBM -> LDS through a 4-slot ring (128 KiB) with global_load_lds issued three
+// k-steps ahead; waits are counted by hand (vmcnt), barriers are raw s_barrier.
 #include "oz2_split.hpp"
 
 namespace oz2 {
@@ -25,14 +30,14 @@ namespace oz2 {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
-constexpr int NTHREADS = 256;
+constexpr int NTHREADS = 512;
 #ifndef OZ2_STAGES
 #define OZ2_STAGES 4
 #endif
 constexpr int STAGES = OZ2_STAGES;  // ring slots; DMA runs STAGES-1 k-steps ahead
-constexpr int SLOT = 2 * PANEL;                 // A panel + B panel
-constexpr int LDS_BYTES = STAGES * SLOT;        // the epilogue reuses 64 KiB of it
-constexpr int GLDS_PER_STEP = 8;                // 16-B LDS-DMA per thread per k-step (4 A + 4 B)
+constexpr int SLOT = 2 * PANEL;     // A panel + B panel
+constexpr int LDS_BYTES = STAGES * SLOT;  // the epilogue reuses 64 KiB of it
+constexpr int GLDS_PER_STEP = 4;          // 1 KiB LDS-DMA pieces per wave per k-step (2 A + 2 B)
 
 struct GemmArgs {
     const int8_t *A;
@@ -43,7 +48,10 @@ struct GemmArgs {
     size_t planeOut, ldo;
     int32_t *rowmax, *colmax;
     int p[OZ2_MAX_MODULI];
-    int barrett[OZ2_MAX_MODULI];
+    int barrett[OZ2_MAX_MODULI];     // floor(2^32/p) - 1 (signed path, reference conv_32i_2_8u)
+    uint32_t minv[OZ2_MAX_MODULI];   // floor(2^32/p)     (biased unsigned path)
+    int bias[OZ2_MAX_MODULI];        // ceil(2^30/p) * p  (accumulator start value, biased path)
+    int biased;                      // |product| <= 2^30 (k_pad <= 2^16): biased path
 };
 
 // One 16-byte-per-lane LDS-DMA: LDS[m0 + lane*16] <- gsrc (per lane).  Issued from inline asm
@@ -59,25 +67,22 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
                  : "=&s"(keep)
                  : "v"(gsrc), "s"(lds_addr)
                  : "memory");
-}
-// sched_barrier(0) after each: hipcc would otherwise move register-only MFMAs across these
-// asm statements (their "memory" clobber does not order them), stretching live ranges
-// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]);
-// the builtin form is visible to the compiler's own waitcnt tracking of its ds_reads.
-template <int N> __device__ __forceinline__ void wait_vmcnt() {
-    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
     __builtin_amdgcn_sched_barrier(0);
 }
-__device__ __forceinline__ void wait_lgkm0() {
-    __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+// s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]);
+// the builtin form is visible to the compiler's own waitcnt tracking of its ds_reads.
+template <int N> __device__ __forceinline__ void wait_vm_lgkm0() {
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (0 << 8) | ((N >> 4) << 14));
     __builtin_amdgcn_sched_barrier(0);
 }
 __device__ __forceinline__ void barrier() {
+    __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// r = x mod p in [0, p): conv_32i_2_8u.hpp:7-56 (modulus 256 = low byte, others Barrett)
+// r = x mod p in [0, p), the value of conv_32i_2_8u.hpp:7-56 (modulus 256 = low byte, others
+// Barrett).  Signed path, any |x| <= 2^31:
 __device__ __forceinline__ uint32_t residue(int x, int p, int barrett, bool p256) {
     if (p256) return (uint32_t)x & 0xffu;
     x -= __mulhi(x, barrett) * p;
@@ -85,32 +90,51 @@ __device__ __forceinline__ uint32_t residue(int x, int p, int barrett, bool p256
     x += (x < 0) * p;
     return (uint32_t)x;
 }
+// Biased path: the accumulator started at bias = ceil(2^30/p)*p (a multiple of p), so for
+// |x| <= 2^30 it holds u = x + bias in [0, 2^31 + p).  With m = floor(2^32/p),
+// q = floor(u*m / 2^32) is floor(u/p) or one less, so u - q*p lies in [0, 2p) and one
+// unsigned min folds it into [0, p).  q < 2^24, so q*p is a full-rate 24-bit multiply.
+// Five VALU ops, no branches, one formula for every modulus including 256.
+__device__ __forceinline__ uint32_t residue_biased(uint32_t u, uint32_t p, uint32_t m) {
+    const uint32_t q = __umulhi(u, m);
+    const uint32_t r = u - __umul24(q, p);
+    return min(r, r - p);
+}
 
-// One half-step (32-deep k-substep) of fragments: 4 row blocks of A, 4 column blocks of B.
-struct Half {
-    v4i a[4];
-    v4i b[4];
+// One k-step of fragments for a wave: 4 row blocks of A, 2 column blocks of B, both 32-deep halves.
+struct Frags {
+    v4i a[2][4];
+    v4i b[2][2];
 };
 
-__device__ __forceinline__ void read_half(Half &h, const int8_t *slot, int s, int wm, int wn, int lane) {
-    const int8_t *la = slot + s * 8192 + (wm * 4) * 1024 + lane * 16;
-    const int8_t *lb = slot + PANEL + s * 8192 + (wn * 4) * 1024 + lane * 16;
+// panel layout [s:2][blk:8][h:2][r:32][16 B]: fragment (s, blk) is the 1 KiB at s*8192 + blk*1024
+__device__ __forceinline__ void read_frags(Frags &f, const int8_t *slot, int wr, int wc, int lane) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        h.a[i] = *reinterpret_cast<const v4i *>(la + i * 1024);
-        h.b[i] = *reinterpret_cast<const v4i *>(lb + i * 1024);
+    for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            f.a[s][i] = *reinterpret_cast<const v4i *>(slot + s * 8192 + (wr * 4 + i) * 1024 + lane * 16);
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+            f.b[s][jj] = *reinterpret_cast<const v4i *>(slot + PANEL + s * 8192 + (wc * 2 + jj) * 1024 + lane * 16);
     }
 }
 
-// 4 MFMAs of row block g (acc[g][0..3]) from one half-step of fragments
-__device__ __forceinline__ void mfma_row(v16i (&acc)[4][4], const Half &h, int g) {
-    if (OZ2_ABLATE == 2) {
+__device__ __forceinline__ void mfma_step(v16i (&acc)[4][2], const Frags &f) {
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[g][j][0] += h.a[g][0] ^ h.b[j][1];
-        return;
-    }
+    for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[g][j] = __builtin_amdgcn_mfma_i32_32x32x32_i8(h.a[g], h.b[j], acc[g][j], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                if (OZ2_ABLATE == 2) {
+                    acc[i][jj][0] += f.a[s][i][0] ^ f.b[s][jj][1];
+                } else {
+                    acc[i][jj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.a[s][i], f.b[s][jj], acc[i][jj], 0, 0, 0);
+                }
+            }
+    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -119,7 +143,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(1024))) int8_t smem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wr = wave >> 2, wc = wave & 3;  // wr doubles as the ping-pong group
     const unsigned j = blockIdx.y;
 
     // XCD-aware, bijective remap: blocks dealt round-robin over the 8 XCDs get
@@ -134,130 +158,108 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     const unsigned idx = wgid - grp * GM * g.ntiles;
     const unsigned tm = grp * GM + idx % gm, tn = idx / gm;
 
-    const int8_t *Ag = g.A + j * g.planeA + (size_t)tm * g.ksteps * PANEL + tid * 16;
-    const int8_t *Bg = g.B + j * g.planeB + (size_t)tn * g.ksteps * PANEL + tid * 16;
+    // LDS-DMA pieces of this wave: 1 KiB blocks {wave, wave + 8} of the A and of the B panel
+    const int8_t *Ag = g.A + j * g.planeA + (size_t)tm * g.ksteps * PANEL + wave * 1024 + lane * 16;
+    const int8_t *Bg = g.B + j * g.planeB + (size_t)tn * g.ksteps * PANEL + wave * 1024 + lane * 16;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
     const uint32_t lds_wave = lds_base + wave * 1024;
-
-    // part 0..3: quarter q of the A panel, 4..7: of the B panel (1 KiB per wave each)
-    auto stage_part = [&](unsigned ks, unsigned slot, int part) {
-        const int8_t *g0 = (part < 4 ? Ag : Bg) + (size_t)ks * PANEL + (part & 3) * 4096;
-        glds16(g0, lds_wave + slot * SLOT + (part < 4 ? 0 : PANEL) + (part & 3) * 4096);
-        __builtin_amdgcn_sched_barrier(0);
-    };
     auto stage = [&](unsigned ks, unsigned slot) {
-#pragma unroll
-        for (int part = 0; part < 8; ++part) stage_part(ks, slot, part);
+        const size_t go = (size_t)ks * PANEL;
+        const uint32_t lo = lds_wave + slot * SLOT;
+        glds16(Ag + go, lo);
+        glds16(Ag + go + 8192, lo + 8192);
+        glds16(Bg + go, lo + PANEL);
+        glds16(Bg + go + 8192, lo + PANEL + 8192);
     };
 
-    v16i acc[4][4];
+    v16i acc[4][2];
+    const int acc0 = (EPI == (int)Epi::RESIDUE && g.biased) ? g.bias[j] : 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = v16i{};
+        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = v16i{} + acc0;  // splat
 
-    // Per k-step t (slot of t landed, half 0 of t in h0):
-    //   issue LDS-DMA of step t+2;  MFMA(h0) || read half 1 of t -> h1;  wait lgkm
-    //   wait vmcnt (step t+1 landed);  barrier
-    //   MFMA(h1) || read half 0 of t+1 -> h0;  wait lgkm
-    // The slot written at step t was last read before the barrier of step t-1.
     const unsigned K = g.ksteps;
     constexpr unsigned D = STAGES - 1;  // prefetch distance in k-steps
-    Half h0, h1;
-    if (K == 0) goto epilogue;
-    // prologue: steps 0..D-1 in flight, wait for step 0
-    for (unsigned s0 = 0; s0 < D; ++s0)
-        if (s0 < K) stage(s0, s0);
-    if (K >= D) wait_vmcnt<GLDS_PER_STEP *(D - 1)>();
-    else wait_vmcnt<0>();
-    barrier();
-    read_half(h0, smem, 0, wm, wn, lane);
-    wait_lgkm0();
-    {
-        unsigned slot_cur = 0, slot_next = 1, slot_issue = D;  // slots of steps t, t+1, t+D
+    static_assert(D == 3, "the drain-loop vmcnt counts assume a 3-step prefetch");
+    if (K > 0) {
+        // prologue: steps 0..D-1 in flight, step 0 landed for every wave, then group 1 falls one
+        // barrier behind.  Barrier accounting (the same for both groups): 1 + 2K + 1 before the epilogue.
+        for (unsigned s0 = 0; s0 < D; ++s0)
+            if (s0 < K) stage(s0, s0);
+        if (K >= D) wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();
+        else wait_vm_lgkm0<0>();
+        barrier();
+        if (wr == 1) barrier();
+
+        // Step t, per wave: load interval (reads of slot t%S, DMA of step t+D into the slot of
+        // step t-1, wait until step t+1 landed and the reads returned), barrier, MFMA interval,
+        // barrier.  RAW: every wave retires its part of step t+1 before the barrier that ends its
+        // load interval of step t; the first read of step t+1 (group 0) follows group 1's next
+        // barrier.  WAR: the slot of step t-1 was last read by group 1 in its previous load
+        // interval, which waited lgkmcnt(0) before its barrier.
+        Frags f;
+        unsigned slot_cur = 0, slot_issue = D % STAGES;
         unsigned t = 0;
-        // Steady state (step t+D exists), branch-free: the 8 LDS-DMA of step t+D are spread one
-        // per 4 MFMAs over both half-steps so their issue cost hides under MFMA execution.  At the
-        // end of half 0, younger than step t+1's DMA are those of steps t+2..t+D-1 (8 each) and the
-        // 4 just issued: vmcnt(8*(D-2)+4).  The slot refilled at step t is that of step t-1, whose
-        // last reads completed before the barrier of step t-1.
-        for (; t + D < K; ++t) {
-            read_half(h1, smem + slot_cur * SLOT, 1, wm, wn, lane);
+        for (; t + D < K; ++t) {  // steady state
+            read_frags(f, smem + slot_cur * SLOT, wr, wc, lane);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                mfma_row(acc, h0, gq);
-                stage_part(t + D, slot_issue, gq);
-            }
-            constexpr int VM = GLDS_PER_STEP * (D - 2) + 4;
-            __builtin_amdgcn_s_waitcnt((VM & 15) | (7 << 4) | (0 << 8) | ((VM >> 4) << 14));  // vmcnt(VM) lgkmcnt(0)
-            __builtin_amdgcn_sched_barrier(0);
+            stage(t + D, slot_issue);
+            wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();
             barrier();
-            read_half(h0, smem + slot_next * SLOT, 0, wm, wn, lane);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) {
-                mfma_row(acc, h1, gq);
-                stage_part(t + D, slot_issue, 4 + gq);
-            }
-            wait_lgkm0();
-            slot_cur = slot_next;
-            slot_next = slot_next == STAGES - 1 ? 0 : slot_next + 1;
+            mfma_step(acc, f);
+            barrier();
+            slot_cur = slot_cur == STAGES - 1 ? 0 : slot_cur + 1;
             slot_issue = slot_issue == STAGES - 1 ? 0 : slot_issue + 1;
         }
-        // drain: nothing left to stage (last D steps)
-        for (; t + 1 < K; ++t) {
-            read_half(h1, smem + slot_cur * SLOT, 1, wm, wn, lane);
+        for (; t < K; ++t) {  // drain: nothing left to stage
+            read_frags(f, smem + slot_cur * SLOT, wr, wc, lane);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) mfma_row(acc, h0, gq);
-            wait_lgkm0();
-            wait_vmcnt<0>();
+            if (t + 2 < K) wait_vm_lgkm0<GLDS_PER_STEP *(D - 2)>();  // D = 3: step t+2 may still fly
+            else wait_vm_lgkm0<0>();
             barrier();
-            read_half(h0, smem + slot_next * SLOT, 0, wm, wn, lane);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int gq = 0; gq < 4; ++gq) mfma_row(acc, h1, gq);
-            wait_lgkm0();
-            slot_cur = slot_next;
-            slot_next = slot_next == STAGES - 1 ? 0 : slot_next + 1;
+            mfma_step(acc, f);
+            barrier();
+            slot_cur = slot_cur == STAGES - 1 ? 0 : slot_cur + 1;
         }
-        // last step
-        read_half(h1, smem + slot_cur * SLOT, 1, wm, wn, lane);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) mfma_row(acc, h0, gq);
-        wait_lgkm0();
-#pragma unroll
-        for (int gq = 0; gq < 4; ++gq) mfma_row(acc, h1, gq);
+        if (wr == 0) barrier();
     }
-epilogue:
     barrier();  // all waves done with the ring before the epilogue reuses it
 
     // accumulator map (32x32 fragments): col = lane & 31, row = (r & 3) + 8*(r >> 2) + 4*(lane >> 5)
     if constexpr (EPI == (int)Epi::RESIDUE) {
-        const int p = g.p[j], bar = g.barrett[j];
-        const bool p256 = (p == 256);  // modulus 256: the low byte (conv_32i_2_8u.hpp:7-20)
+        const int p = g.p[j];
         uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
+        // residues of the 4 x 2 fragments -> LDS, one fragment at a time (bounded VGPR use)
+        auto park = [&](auto &&res) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj) {
-                const int col = wn * 128 + jj * 32 + (lane & 31);
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int col = wc * 64 + jj * 32 + (lane & 31);
 #pragma unroll
-                for (int gq = 0; gq < 4; ++gq) {
-                    uint32_t w = 0;
+                    for (int gq = 0; gq < 4; ++gq) {
+                        uint32_t w = 0;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) w |= residue(acc[i][jj][4 * gq + e], p, bar, p256) << (8 * e);
-                    const int rdw = wm * 32 + i * 8 + 2 * gq + (lane >> 5);
-                    lo[col * 64 + (rdw ^ (col & 31))] = w;
+                        for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][4 * gq + e]) << (8 * e);
+                        const int rdw = wr * 32 + i * 8 + 2 * gq + (lane >> 5);
+                        lo[col * 64 + (rdw ^ (col & 31))] = w;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
                 }
-                __builtin_amdgcn_sched_barrier(0);  // one fragment at a time: bounded VGPR use
-            }
+        };
+        if (g.biased) {
+            const uint32_t m = g.minv[j];
+            park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
+        } else {
+            const int bar = g.barrett[j];
+            const bool p256 = (p == 256);  // modulus 256: the low byte (conv_32i_2_8u.hpp:7-20)
+            park([&](int x) { return residue(x, p, bar, p256); });
+        }
         __syncthreads();
         uint8_t *out = static_cast<uint8_t *>(g.out) + j * g.planeOut + (size_t)tn * 256 * g.ldo + (size_t)tm * 256;
 #pragma unroll
-        for (int it = 0; it < 16; ++it) {
+        for (int it = 0; it < 4096 / NTHREADS; ++it) {
             const int chunk = tid + NTHREADS * it;
             const int col = chunk >> 4, qd = chunk & 15;
             const int x = col & 31;
@@ -270,8 +272,10 @@ epilogue:
     } else if constexpr (EPI == (int)Epi::BOUND) {
         int32_t *rmax = reinterpret_cast<int32_t *>(smem);
         int32_t *cmax = rmax + 256;
-        rmax[tid] = 0;
-        cmax[tid] = 0;
+        if (tid < 256) {
+            rmax[tid] = 0;
+            cmax[tid] = 0;
+        }
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -279,34 +283,36 @@ epilogue:
             for (int rr = 0; rr < 16; ++rr) {
                 int v = 0;
 #pragma unroll
-                for (int jj = 0; jj < 4; ++jj) v = max(v, abs(acc[i][jj][rr]));
+                for (int jj = 0; jj < 2; ++jj) v = max(v, abs(acc[i][jj][rr]));
 #pragma unroll
                 for (int d = 16; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 32));
-                if ((lane & 31) == 0) atomicMax(&rmax[wm * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5)], v);
+                if ((lane & 31) == 0) atomicMax(&rmax[wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5)], v);
             }
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
+        for (int jj = 0; jj < 2; ++jj) {
             int v = 0;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int rr = 0; rr < 16; ++rr) v = max(v, abs(acc[i][jj][rr]));
             v = max(v, __shfl_xor(v, 32));
-            if (lane < 32) atomicMax(&cmax[wn * 128 + jj * 32 + lane], v);
+            if (lane < 32) atomicMax(&cmax[wc * 64 + jj * 32 + lane], v);
         }
         __syncthreads();
-        atomicMax(&g.rowmax[tm * 256 + tid], rmax[tid]);
-        atomicMax(&g.colmax[tn * 256 + tid], cmax[tid]);
+        if (tid < 256) {
+            atomicMax(&g.rowmax[tm * 256 + tid], rmax[tid]);
+            atomicMax(&g.colmax[tn * 256 + tid], cmax[tid]);
+        }
     } else {  // RAW int32 (plane 0): validation path
         int32_t *out = static_cast<int32_t *>(g.out);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int jj = 0; jj < 4; ++jj)
+            for (int jj = 0; jj < 2; ++jj)
 #pragma unroll
                 for (int rr = 0; rr < 16; ++rr) {
-                    const size_t row = (size_t)tm * 256 + wm * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
-                    const size_t col = (size_t)tn * 256 + wn * 128 + jj * 32 + (lane & 31);
+                    const size_t row = (size_t)tm * 256 + wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+                    const size_t col = (size_t)tn * 256 + wc * 64 + jj * 32 + (lane & 31);
                     out[col * g.ldo + row] = acc[i][jj][rr];
                 }
     }
@@ -327,9 +333,14 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     g.ldo = L.m_pad;
     g.rowmax = rowmax;
     g.colmax = colmax;
+    // |int8 product| <= 2^14 * k_pad: the biased residue path needs <= 2^30
+    g.biased = L.k_pad <= ((size_t)1 << 16) ? 1 : 0;
     for (int i = 0; i < OZ2_MAX_MODULI; ++i) {
         g.p[i] = MP.p[i];
         g.barrett[i] = MP.barrett[i];
+        const uint32_t p = MP.p[i] > 0 ? (uint32_t)MP.p[i] : 256u;
+        g.minv[i] = (uint32_t)((((uint64_t)1) << 32) / p);
+        g.bias[i] = (int)(((((uint64_t)1) << 30) + p - 1) / p * p);
     }
     dim3 grid((unsigned)(L.mtiles * L.ntiles), nplanes);
     switch (epi) {
