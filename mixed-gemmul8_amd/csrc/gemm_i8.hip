@@ -58,7 +58,7 @@ struct GemmArgs {
 // so the compiler neither waits for it nor reorders it; completion is counted with vmcnt by hand.
 // M0 is compiler-reserved: saved and restored inside the statement.
 #ifndef OZ2_ABLATE
-#define OZ2_ABLATE 0  // probe builds only: 1 = no LDS-DMA in the main loop, 2 = no MFMA
+#define OZ2_ABLATE 0  // probe builds only: 1 = no LDS-DMA in the main loop, 2 = no MFMA, 3 = no LDS reads
 #endif
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
     if (OZ2_ABLATE == 1) return;
@@ -74,6 +74,15 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
 template <int N> __device__ __forceinline__ void wait_vm_lgkm0() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (0 << 8) | ((N >> 4) << 14));
     __builtin_amdgcn_sched_barrier(0);
+}
+// drain: wait until at most `younger` k-steps of this wave's LDS-DMA remain in flight
+template <int PER_STEP> __device__ __forceinline__ void wait_steps_lgkm0(int younger) {
+    switch (younger) {
+    case 0: wait_vm_lgkm0<0>(); break;
+    case 1: wait_vm_lgkm0<PER_STEP>(); break;
+    case 2: wait_vm_lgkm0<2 * PER_STEP>(); break;
+    default: wait_vm_lgkm0<3 * PER_STEP>(); break;
+    }
 }
 __device__ __forceinline__ void barrier() {
     __builtin_amdgcn_sched_barrier(0);
@@ -109,6 +118,16 @@ struct Frags {
 
 // panel layout [s:2][blk:8][h:2][r:32][16 B]: fragment (s, blk) is the 1 KiB at s*8192 + blk*1024
 __device__ __forceinline__ void read_frags(Frags &f, const int8_t *slot, int wr, int wc, int lane) {
+    if (OZ2_ABLATE == 3 || OZ2_ABLATE == 4) {  // probe: no LDS reads (operands = slot address bits)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f.a[s][i] = v4i{} + (int)(uintptr_t)slot + i;
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) f.b[s][jj] = v4i{} + (int)(uintptr_t)slot + jj;
+        }
+        return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
 #pragma unroll
@@ -128,7 +147,7 @@ __device__ __forceinline__ void mfma_step(v16i (&acc)[4][2], const Frags &f) {
         for (int i = 0; i < 4; ++i)
 #pragma unroll
             for (int jj = 0; jj < 2; ++jj) {
-                if (OZ2_ABLATE == 2) {
+                if (OZ2_ABLATE == 2 || OZ2_ABLATE == 4) {
                     acc[i][jj][0] += f.a[s][i][0] ^ f.b[s][jj][1];
                 } else {
                     acc[i][jj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.a[s][i], f.b[s][jj], acc[i][jj], 0, 0, 0);
@@ -136,6 +155,105 @@ __device__ __forceinline__ void mfma_step(v16i (&acc)[4][2], const Frags &f) {
             }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
+}
+
+// Epilogues over the 8 compute waves' accumulators (active = this wave holds a 128 x 64 block;
+// every thread of the block must call it: it contains block barriers).
+template <int EPI>
+__device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], int8_t *smem, int tid, int lane, int wr,
+                                         int wc, unsigned tm, unsigned tn, unsigned j, bool active) {
+    // accumulator map (32x32 fragments): col = lane & 31, row = (r & 3) + 8*(r >> 2) + 4*(lane >> 5)
+    if constexpr (EPI == (int)Epi::RESIDUE) {
+        const int p = g.p[j];
+        uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
+        // residues of the 4 x 2 fragments -> LDS, one fragment at a time (bounded VGPR use)
+        auto park = [&](auto &&res) {
+            if (!active) return;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) {
+                    const int col = wc * 64 + jj * 32 + (lane & 31);
+#pragma unroll
+                    for (int gq = 0; gq < 4; ++gq) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][4 * gq + e]) << (8 * e);
+                        const int rdw = wr * 32 + i * 8 + 2 * gq + (lane >> 5);
+                        lo[col * 64 + (rdw ^ (col & 31))] = w;
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+        };
+        if (g.biased) {
+            const uint32_t m = g.minv[j];
+            park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
+        } else {
+            const int bar = g.barrett[j];
+            const bool p256 = (p == 256);  // modulus 256: the low byte (conv_32i_2_8u.hpp:7-20)
+            park([&](int x) { return residue(x, p, bar, p256); });
+        }
+        __syncthreads();
+        uint8_t *out = static_cast<uint8_t *>(g.out) + j * g.planeOut + (size_t)tn * 256 * g.ldo + (size_t)tm * 256;
+#pragma unroll
+        for (int it = 0; it < 4096 / 512; ++it) {
+            if (tid >= 512) break;
+            const int chunk = tid + 512 * it;
+            const int col = chunk >> 4, qd = chunk & 15;
+            const int x = col & 31;
+            const uint4 v = *reinterpret_cast<const uint4 *>(lo + col * 64 + ((4 * qd) ^ (x & ~3)));
+            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+            const int pm = x & 3;
+            *reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd) =
+                make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+        }
+    } else if constexpr (EPI == (int)Epi::BOUND) {
+        int32_t *rmax = reinterpret_cast<int32_t *>(smem);
+        int32_t *cmax = rmax + 256;
+        if (tid < 256) {
+            rmax[tid] = 0;
+            cmax[tid] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4 && active; ++i)
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) {
+                int v = 0;
+#pragma unroll
+                for (int jj = 0; jj < 2; ++jj) v = max(v, abs(acc[i][jj][rr]));
+#pragma unroll
+                for (int d = 16; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 32));
+                if ((lane & 31) == 0) atomicMax(&rmax[wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5)], v);
+            }
+#pragma unroll
+        for (int jj = 0; jj < 2 && active; ++jj) {
+            int v = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) v = max(v, abs(acc[i][jj][rr]));
+            v = max(v, __shfl_xor(v, 32));
+            if (lane < 32) atomicMax(&cmax[wc * 64 + jj * 32 + lane], v);
+        }
+        __syncthreads();
+        if (tid < 256) {
+            atomicMax(&g.rowmax[tm * 256 + tid], rmax[tid]);
+            atomicMax(&g.colmax[tn * 256 + tid], cmax[tid]);
+        }
+    } else if (active) {  // RAW int32 (plane 0): validation path
+        int32_t *out = static_cast<int32_t *>(g.out);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                for (int rr = 0; rr < 16; ++rr) {
+                    const size_t row = (size_t)tm * 256 + wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
+                    const size_t col = (size_t)tn * 256 + wc * 64 + jj * 32 + (lane & 31);
+                    out[col * g.ldo + row] = acc[i][jj][rr];
+                }
+    }
 }
 
 template <int EPI>
@@ -181,14 +299,14 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
 
     const unsigned K = g.ksteps;
     constexpr unsigned D = STAGES - 1;  // prefetch distance in k-steps
-    static_assert(D == 3, "the drain-loop vmcnt counts assume a 3-step prefetch");
+    static_assert(D >= 2 && D <= 5, "drain-loop vmcnt cases cover prefetch distances 2..5");
     if (K > 0) {
         // prologue: steps 0..D-1 in flight, step 0 landed for every wave, then group 1 falls one
         // barrier behind.  Barrier accounting (the same for both groups): 1 + 2K + 1 before the epilogue.
         for (unsigned s0 = 0; s0 < D; ++s0)
             if (s0 < K) stage(s0, s0);
         if (K >= D) wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();
-        else wait_vm_lgkm0<0>();
+        else wait_steps_lgkm0<GLDS_PER_STEP>((int)K - 1);
         barrier();
         if (wr == 1) barrier();
 
@@ -215,8 +333,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
         for (; t < K; ++t) {  // drain: nothing left to stage
             read_frags(f, smem + slot_cur * SLOT, wr, wc, lane);
             __builtin_amdgcn_sched_barrier(0);
-            if (t + 2 < K) wait_vm_lgkm0<GLDS_PER_STEP *(D - 2)>();  // D = 3: step t+2 may still fly
-            else wait_vm_lgkm0<0>();
+            wait_steps_lgkm0<GLDS_PER_STEP>(t + 2 < K ? (int)(K - t - 2) : 0);  // steps t+2..K-1 may fly
             barrier();
             mfma_step(acc, f);
             barrier();
@@ -226,97 +343,9 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     }
     barrier();  // all waves done with the ring before the epilogue reuses it
 
-    // accumulator map (32x32 fragments): col = lane & 31, row = (r & 3) + 8*(r >> 2) + 4*(lane >> 5)
-    if constexpr (EPI == (int)Epi::RESIDUE) {
-        const int p = g.p[j];
-        uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
-        // residues of the 4 x 2 fragments -> LDS, one fragment at a time (bounded VGPR use)
-        auto park = [&](auto &&res) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int col = wc * 64 + jj * 32 + (lane & 31);
-#pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) {
-                        uint32_t w = 0;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][4 * gq + e]) << (8 * e);
-                        const int rdw = wr * 32 + i * 8 + 2 * gq + (lane >> 5);
-                        lo[col * 64 + (rdw ^ (col & 31))] = w;
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-        };
-        if (g.biased) {
-            const uint32_t m = g.minv[j];
-            park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
-        } else {
-            const int bar = g.barrett[j];
-            const bool p256 = (p == 256);  // modulus 256: the low byte (conv_32i_2_8u.hpp:7-20)
-            park([&](int x) { return residue(x, p, bar, p256); });
-        }
-        __syncthreads();
-        uint8_t *out = static_cast<uint8_t *>(g.out) + j * g.planeOut + (size_t)tn * 256 * g.ldo + (size_t)tm * 256;
-#pragma unroll
-        for (int it = 0; it < 4096 / NTHREADS; ++it) {
-            const int chunk = tid + NTHREADS * it;
-            const int col = chunk >> 4, qd = chunk & 15;
-            const int x = col & 31;
-            const uint4 v = *reinterpret_cast<const uint4 *>(lo + col * 64 + ((4 * qd) ^ (x & ~3)));
-            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
-            const int pm = x & 3;
-            *reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd) =
-                make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
-        }
-    } else if constexpr (EPI == (int)Epi::BOUND) {
-        int32_t *rmax = reinterpret_cast<int32_t *>(smem);
-        int32_t *cmax = rmax + 256;
-        if (tid < 256) {
-            rmax[tid] = 0;
-            cmax[tid] = 0;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int rr = 0; rr < 16; ++rr) {
-                int v = 0;
-#pragma unroll
-                for (int jj = 0; jj < 2; ++jj) v = max(v, abs(acc[i][jj][rr]));
-#pragma unroll
-                for (int d = 16; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 32));
-                if ((lane & 31) == 0) atomicMax(&rmax[wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5)], v);
-            }
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            int v = 0;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int rr = 0; rr < 16; ++rr) v = max(v, abs(acc[i][jj][rr]));
-            v = max(v, __shfl_xor(v, 32));
-            if (lane < 32) atomicMax(&cmax[wc * 64 + jj * 32 + lane], v);
-        }
-        __syncthreads();
-        if (tid < 256) {
-            atomicMax(&g.rowmax[tm * 256 + tid], rmax[tid]);
-            atomicMax(&g.colmax[tn * 256 + tid], cmax[tid]);
-        }
-    } else {  // RAW int32 (plane 0): validation path
-        int32_t *out = static_cast<int32_t *>(g.out);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
-#pragma unroll
-                for (int rr = 0; rr < 16; ++rr) {
-                    const size_t row = (size_t)tm * 256 + wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
-                    const size_t col = (size_t)tn * 256 + wc * 64 + jj * 32 + (lane & 31);
-                    out[col * g.ldo + row] = acc[i][jj][rr];
-                }
-    }
+    epilogue<EPI>(g, acc, smem, tid, lane, wr, wc, tm, tn, j, true);
 }
+
 
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
              int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st) {

@@ -34,7 +34,7 @@ int main(int argc, char **argv) {
         (void)hipEventSynchronize(e1);
         float ms;
         (void)hipEventElapsedTime(&ms, e0, e1);
-        if (rep) printf("ablate=%d stages=%d N=%u k=%zu %s: %.3f ms  %.0f TOPS\n", OZ2_ABLATE, OZ2_STAGES, N, k,
+        if (rep) printf("%s stages=%d N=%u k=%zu %s: %.3f ms  %.0f TOPS\n", argv[0], OZ2_STAGES, N, k,
                         rnd ? "rand" : "const", ms, 2.0 * m * n * k * N / ms / 1e9);
     }
     return 0;
