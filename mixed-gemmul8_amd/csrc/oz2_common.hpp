@@ -148,6 +148,25 @@ __device__ __forceinline__ int mod8_f64(double x, int p, double rinv, float rinv
     t = __builtin_fmaf(__builtin_rintf(t * rinvf), pf, t);
     return (int)t;
 }
+// Steps 2-3 of mod8_f64 on two values at once: packed f32 multiply / add / fma, with
+// round-to-nearest-even by the 1.5*2^23 shift ((y + c) - c == rintf(y) for |y| <= 2^22; here
+// |y| < 2^15), so the result is bit-identical to the scalar form above.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v mod8_tail_x2(f2v t, float rinvf, float pf) {
+    const f2v c = {12582912.0f, 12582912.0f};
+    const f2v r = {rinvf, rinvf}, q = {pf, pf};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        f2v y = t * r;
+        y = (y + c) - c;
+        t = __builtin_elementwise_fma(y, q, t);
+    }
+    return t;
+}
+__device__ __forceinline__ float mod8_head_f64(double x, int p, double rinv) {
+    return __double2float_rn(__builtin_fma(__builtin_rint(x * rinv), -(double)p, x));
+}
+
 __device__ __forceinline__ int mod8_f32(float x, int p, float rinvf) {
     const float pf = -(float)p;
     float t = __builtin_fmaf(__builtin_rintf(x * rinvf), pf, x);

@@ -294,23 +294,45 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
         const int p = MP.p[j];
         const double rd = MP.rinv_d[j];
         const float rf = MP.rinv_f[j];
+        // residues of the 16 elements: mod8_f64 (scaling.hpp:215-223) as its f64 head per element
+        // and its two f32 steps on packed pairs; mod8_f32 (:225-230) per element
+        int rr[16], ri[16];
+        if constexpr (std::is_same<R, double>::value) {
+            float tr[16], tim[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                tr[q] = mod8_head_f64(yr[q], p, rd);
+                tim[q] = CPLX ? mod8_head_f64(yi[q], p, rd) : 0.0f;
+            }
+            const float pf = -(float)p;
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+                const f2v a = mod8_tail_x2(f2v{tr[q], tr[q + 1]}, rf, pf);
+                rr[q] = (int)a.x;
+                rr[q + 1] = (int)a.y;
+                if (CPLX) {
+                    const f2v b = mod8_tail_x2(f2v{tim[q], tim[q + 1]}, rf, pf);
+                    ri[q] = (int)b.x;
+                    ri[q + 1] = (int)b.y;
+                } else {
+                    ri[q] = ri[q + 1] = 0;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                rr[q] = mod8_f32(yr[q], p, rf);
+                ri[q] = CPLX ? mod8_f32(yi[q], p, rf) : 0;
+            }
+        }
         uint32_t wr[4], wi[4];
 #pragma unroll
         for (int d = 0; d < 4; ++d) {
             uint32_t ar = 0, ai = 0;
 #pragma unroll
             for (int b = 0; b < 4; ++b) {
-                const int q = 4 * d + b;
-                int rr, ri = 0;
-                if constexpr (std::is_same<R, double>::value) {
-                    rr = mod8_f64(yr[q], p, rd, rf);
-                    if (CPLX) ri = mod8_f64(yi[q], p, rd, rf);
-                } else {
-                    rr = mod8_f32(yr[q], p, rf);
-                    if (CPLX) ri = mod8_f32(yi[q], p, rf);
-                }
-                ar |= ((uint32_t)rr & 0xffu) << (8 * b);
-                ai |= ((uint32_t)ri & 0xffu) << (8 * b);
+                ar |= ((uint32_t)rr[4 * d + b] & 0xffu) << (8 * b);
+                ai |= ((uint32_t)ri[4 * d + b] & 0xffu) << (8 * b);
             }
             wr[d] = ar;
             wi[d] = ai;
