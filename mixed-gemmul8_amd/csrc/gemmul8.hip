@@ -20,6 +20,7 @@ namespace oz2 {
 
 struct Call {
     OperandDesc A, B;
+    int ctype;
     size_t m, n, k;
     unsigned N;
     bool fast;
@@ -120,7 +121,9 @@ static void phase_bound(const Call &c, const Views &v) {
     split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
     split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.st);
     split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
-    split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.st);
+    // big-matrix B magnitudes carry the reference's tail defect; classic / Karatsuba do not
+    split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.st,
+                 c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE);
     (void)hipMemsetAsync(v.bound, 0, (L.m_pad + L.n_pad) * sizeof(int32_t), c.st);
     gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
 }
@@ -138,7 +141,7 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
     } else {
         const float log2M = oz2_log2M_accu[c.N - 2];
         if (!bound_ready) phase_bound(c, v);
-        split_finalize_accurate(v.sft0, v.bound, c.m, log2M, v.sftA, c.st);
+        split_finalize_accurate(v.sft0, v.bound, c.m, log2M, v.sftA, c.st, c.cplx);
         split_finalize_accurate(v.sft0 + L.m_pad, v.bound + L.m_pad, c.n, log2M, v.sftB, c.st);
     }
     const ModParams SP = sub_mod_params(c.N, j0, j1);
@@ -216,22 +219,24 @@ static int prepare(void *stream, int op_a, int op_b, size_t m, size_t n, size_t 
     if (ta < 0 || ta > 3 || tb < 0 || tb > 3 || tc < 0 || tc > 3) return GEMMUL8_E_TYPES;
     const bool cp = dt_cplx(ta);
     if (dt_cplx(tb) != cp || dt_cplx(tc) != cp) return GEMMUL8_E_TYPES;
-    if (cp && ctype != GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE) {
-        if (ctype == GEMMUL8_COMPLEX_CLASSIC_MULT || ctype == GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_UNSUPPORTED;
+    // the three complex compute types compute the same residues of Re(AB) and Im(AB): one engine
+    // (big-matrix products) serves all of them; only the accurate-mode bound differs (see phase_bound)
+    if (cp && !(ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE || ctype == GEMMUL8_COMPLEX_CLASSIC_MULT ||
+                ctype == GEMMUL8_COMPLEX_KARATSUBA_MULT))
         return GEMMUL8_E_TYPES;
-    }
     if (!cp && ctype != GEMMUL8_REAL_DEFAULT) return GEMMUL8_E_TYPES;
     // output precision is the higher of the inputs' in every reference specialization (gemmul8.hpp:49-287)
     if (!cp && !(tc == GEMMUL8_R_64F || tc == GEMMUL8_R_32F)) return GEMMUL8_E_TYPES;
     if (op_a < 0 || op_a > 2 || op_b < 0 || op_b > 2) return GEMMUL8_E_OP;
-    if (cp && (op_a != GEMMUL8_OP_N || op_b != GEMMUL8_OP_N)) return GEMMUL8_E_UNSUPPORTED;
-    if (cp && !fast) return GEMMUL8_E_UNSUPPORTED;
+    // complex accurate mode is restated for op N x op N (scaling.hpp:3138-3245, 3247-3368)
+    if (cp && !fast && (op_a != GEMMUL8_OP_N || op_b != GEMMUL8_OP_N)) return GEMMUL8_E_UNSUPPORTED;
     const size_t kr = cp ? 2 * round_up(k, KSTEP) : round_up(k, KSTEP);
     if (kr > ((size_t)1 << 17)) return GEMMUL8_E_SIZE;
     const bool ta_t = op_a != GEMMUL8_OP_N, tb_t = op_b != GEMMUL8_OP_N;
     if (lda < (ta_t ? k : m) || ldb < (tb_t ? n : k) || ldc < m) return GEMMUL8_E_SIZE;
-    c.A = OperandDesc{A, lda, ta_t, dt_dbl(ta), cp};
-    c.B = OperandDesc{B, ldb, !tb_t, dt_dbl(tb), cp};
+    c.A = OperandDesc{A, lda, ta_t, dt_dbl(ta), cp, cp && op_a == GEMMUL8_OP_C};
+    c.B = OperandDesc{B, ldb, !tb_t, dt_dbl(tb), cp, cp && op_b == GEMMUL8_OP_C};
+    c.ctype = ctype;
     c.m = m; c.n = n; c.k = k; c.N = N;
     c.fast = fast != 0;
     c.cplx = cp;
@@ -300,8 +305,7 @@ int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k
 int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, void *work,
                      unsigned mod_begin, unsigned mod_end) {
     if (num_moduli < 2 || num_moduli > 20 || mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
-    if (compute_type != GEMMUL8_REAL_DEFAULT && compute_type != GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE)
-        return GEMMUL8_E_UNSUPPORTED;
+    if (compute_type < GEMMUL8_REAL_DEFAULT || compute_type > GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_TYPES;
     if (m == 0 || n == 0) return GEMMUL8_OK;
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -334,7 +338,7 @@ int gemmul8_recombine(void *stream, size_t m, size_t n, size_t k, unsigned num_m
     if (type_c < 0 || type_c > 3) return GEMMUL8_E_TYPES;
     const bool cp = compute_type != GEMMUL8_REAL_DEFAULT;
     if (cp != oz2::dt_cplx(type_c)) return GEMMUL8_E_TYPES;
-    if (cp && compute_type != GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE) return GEMMUL8_E_UNSUPPORTED;
+    if (compute_type < GEMMUL8_REAL_DEFAULT || compute_type > GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_TYPES;
     if (ldc < m) return GEMMUL8_E_SIZE;
     if (m == 0 || n == 0) return GEMMUL8_OK;
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, cp);

@@ -13,6 +13,7 @@ struct OperandDesc {
     bool contig;
     bool dbl;      // real part is f64 (else f32)
     bool cplx;
+    bool conj;     // op C of a complex operand
 };
 
 // ---- split.hip ----
@@ -21,10 +22,13 @@ struct OperandDesc {
 void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool accurate, float log2M, int16_t *out,
                  hipStream_t st);
 // mode 0: N residue planes from sft (reference convention -shift); mode 1: 6-bit magnitudes from sft0
+// btail_quirk: accurate-mode big-matrix B magnitudes with the reference's tail defect (see split.hip)
 void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
-                  size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st);
+                  size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st,
+                  bool btail_quirk = false);
+// cplx_rows: complex A bound of row v = max(bound[v], bound[v + nvec]) (scaling.hpp:2561-2588)
 void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
-                             hipStream_t st);
+                             hipStream_t st, bool cplx_rows = false);
 
 // ---- gemm_i8.hip ----
 enum class Epi : int { RESIDUE = 0, BOUND = 1, RAW = 2 };

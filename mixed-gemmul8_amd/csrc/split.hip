@@ -19,6 +19,8 @@
 
 namespace oz2 {
 
+enum : int { ENC_CONJ = 1, ENC_BTAIL = 2 };
+
 template <typename R> __device__ __forceinline__ R fma_ru(R a, R b, R c);
 template <> __device__ __forceinline__ double fma_ru<double>(double a, double b, double c) { return __fma_ru(a, b, c); }
 template <> __device__ __forceinline__ float fma_ru<float>(float a, float b, float c) { return __fmaf_ru(a, b, c); }
@@ -203,13 +205,17 @@ __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict_
 //   MODE 1: 6-bit magnitudes ceil(|x| * 2^sft0), 1 plane (accurate-mode bound)
 // Complex A (IS_A): row v <- [re, -im], row v+m <- [im, re]  (scaling.hpp:753-838)
 // Complex B:        col v <- [re; im]                           (scaling.hpp:1150-1230)
+// flags: ENC_CONJ (op C: the imaginary part enters negated, scaling.hpp:840-1089,
+// 1232-1498); ENC_BTAIL (accurate mode, big-matrix B: the reference's tail loop
+// stores the last k mod 4 imaginary magnitudes outside the column, leaving them 0 in
+// the bound product -- extract_B8i_kernel_bigmatrix, scaling.hpp:2313-2321).
 // ------------------------------------------------------------------
 template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
 __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__restrict__ X, size_t ld, size_t nvec,
                                                                    size_t len, const int16_t *__restrict__ sft,
                                                                    int8_t *__restrict__ out, size_t plane,
                                                                    size_t ksteps, size_t kblk, size_t vmax,
-                                                                   ModParams MP) {
+                                                                   int flags, ModParams MP) {
     constexpr int KT = CPLX ? 32 : 64;
     constexpr int NT = CPLX ? 128 : 256;
     constexpr int NC = CPLX ? 2 : 1;
@@ -249,7 +255,7 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
         int vl, el;
         if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
         tile[el][vl][0] = lre[i];
-        if (CPLX) tile[el][vl][NC - 1] = lim[i];
+        if (CPLX) tile[el][vl][NC - 1] = (flags & ENC_CONJ) ? -lim[i] : lim[i];
     }
     __syncthreads();
 
@@ -269,27 +275,64 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
             yi[q] = trunc(scalbn(im, s));
         } else {
             yr[q] = scalbn(fabs(re), s);
+            yi[q] = scalbn(fabs(im), s);
         }
-    }
-
-    if (MODE == 1) {
-        uint32_t w[4];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) {
-            uint32_t acc = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int q = 4 * d + b;
-                const int val = std::is_same<R, double>::value ? __double2int_ru((double)yr[q]) : __float2int_ru((float)yr[q]);
-                acc |= ((uint32_t)val & 0xffu) << (8 * b);
-            }
-            w[d] = acc;
-        }
-        *reinterpret_cast<uint4 *>(out + panel_offset(v, kk, ksteps)) = make_uint4(w[0], w[1], w[2], w[3]);
-        return;
     }
 
     const bool top = v < nvec || !CPLX || !IS_A;  // complex A: rows >= m only emit their (zero) bottom copy
+    // one plane of slices: real -> (v, kk); complex A -> [wr, -wi] / [wi, wr]; complex B -> [wr; wi]
+    auto emit = [&](int8_t *o, const uint32_t (&wr)[4], const uint32_t (&wi)[4]) {
+        if (!CPLX) {
+            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+        } else if (IS_A) {
+            // -im as bytes: per-byte two's complement negation
+            uint32_t ni[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                uint32_t r = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) r |= ((0u - ((wi[d] >> (8 * b)) & 0xffu)) & 0xffu) << (8 * b);
+                ni[d] = r;
+            }
+            const size_t vb = v + nvec;  // bottom row (v + m)
+            if (top) {
+                *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+                *reinterpret_cast<uint4 *>(o + panel_offset(v, kblk + kk, ksteps)) = make_uint4(ni[0], ni[1], ni[2], ni[3]);
+            }
+            if (vb < vmax) {
+                *reinterpret_cast<uint4 *>(o + panel_offset(vb, kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
+                *reinterpret_cast<uint4 *>(o + panel_offset(vb, kblk + kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+            }
+        } else {
+            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+            *reinterpret_cast<uint4 *>(o + panel_offset(v, kblk + kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
+        }
+    };
+
+    if (MODE == 1) {
+        const size_t tail = (flags & ENC_BTAIL) ? (len & ~(size_t)3) : len;
+        uint32_t wr[4], wi[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            uint32_t ar = 0, ai = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int q = 4 * d + b;
+                const int vr = std::is_same<R, double>::value ? __double2int_ru((double)yr[q]) : __float2int_ru((float)yr[q]);
+                ar |= ((uint32_t)vr & 0xffu) << (8 * b);
+                if (CPLX) {
+                    int vi = std::is_same<R, double>::value ? __double2int_ru((double)yi[q]) : __float2int_ru((float)yi[q]);
+                    if (kk + q >= tail) vi = 0;
+                    ai |= ((uint32_t)vi & 0xffu) << (8 * b);
+                }
+            }
+            wr[d] = ar;
+            wi[d] = ai;
+        }
+        emit(out, wr, wi);
+        return;
+    }
+
     for (unsigned j = 0; j < MP.N; ++j) {
         const int p = MP.p[j];
         const double rd = MP.rinv_d[j];
@@ -337,41 +380,16 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
             wr[d] = ar;
             wi[d] = ai;
         }
-        int8_t *o = out + (size_t)j * plane;
-        if (!CPLX) {
-            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
-        } else if (IS_A) {
-            // -im as bytes: per-byte two's complement negation
-            uint32_t ni[4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                uint32_t r = 0;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) r |= ((0u - ((wi[d] >> (8 * b)) & 0xffu)) & 0xffu) << (8 * b);
-                ni[d] = r;
-            }
-            const size_t vb = v + nvec;  // bottom row (v + m)
-            if (top) {
-                *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
-                *reinterpret_cast<uint4 *>(o + panel_offset(v, kblk + kk, ksteps)) = make_uint4(ni[0], ni[1], ni[2], ni[3]);
-            }
-            if (vb < vmax) {
-                *reinterpret_cast<uint4 *>(o + panel_offset(vb, kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
-                *reinterpret_cast<uint4 *>(o + panel_offset(vb, kblk + kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
-            }
-        } else {
-            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
-            *reinterpret_cast<uint4 *>(o + panel_offset(v, kblk + kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
-        }
+        emit(out + (size_t)j * plane, wr, wi);
     }
 }
 
 // accurate mode: sft = sft0 + floor_rd(-0.51*log2(amax) + log2M)  (int8tc::compute_sft, scaling.hpp:1504-1506)
 __global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, const int32_t *__restrict__ bound,
-                                             size_t nvec, float log2M, int16_t *__restrict__ sft_out) {
+                                             size_t nvec, float log2M, int16_t *__restrict__ sft_out, int cplx_rows) {
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nvec) return;
-    const int amax = bound[v];
+    const int amax = cplx_rows ? max(bound[v], bound[v + nvec]) : bound[v];
     const int s = (int)sft0[v] + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
     sft_out[v] = (int16_t)(-s);
 }
@@ -400,12 +418,12 @@ static void launch_stats(const void *X, size_t ld, bool contig, size_t len, size
 template <typename R, bool CPLX, bool IS_A>
 static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, size_t len, const int16_t *sft,
                           int8_t *out, size_t plane, const Layout &L, size_t vpad_grid, size_t vmax, int mode,
-                          const ModParams &MP, hipStream_t st) {
+                          int flags, const ModParams &MP, hipStream_t st) {
     constexpr int KT = CPLX ? 32 : 64;
     constexpr int NT = CPLX ? 128 : 256;
     const R *x = static_cast<const R *>(X);
     dim3 grid((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
-#define OZ2_EN(cg, md) encode_kernel<R, CPLX, cg, IS_A, md><<<grid, dim3(NT), 0, st>>>(x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, MP)
+#define OZ2_EN(cg, md) encode_kernel<R, CPLX, cg, IS_A, md><<<grid, dim3(NT), 0, st>>>(x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP)
     if (contig) { if (mode == 0) OZ2_EN(true, 0); else OZ2_EN(true, 1); }
     else { if (mode == 0) OZ2_EN(false, 0); else OZ2_EN(false, 1); }
 #undef OZ2_EN
@@ -423,13 +441,14 @@ void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool acc
 }
 
 void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
-                  size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st) {
+                  size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st, bool btail_quirk) {
+    const int flags = (d.conj ? ENC_CONJ : 0) | (btail_quirk && mode == 1 && !is_A ? ENC_BTAIL : 0);
     // grid extent over vectors: padded rows/cols get zero slices; complex A covers
     // [0, m_pad - m) so that rows [2m, m_pad) are zeroed through their bottom copy
     size_t vpad = is_A ? (d.cplx ? L.m_pad - L.m : L.m_pad) : L.n_pad;
     vpad = round_up(vpad, 64);
     const size_t vmax = is_A ? L.m_pad : L.n_pad;
-#define OZ2_LE(R, C, A) launch_encode<R, C, A>(d.ptr, d.ld, d.contig, nvec, len, sft, out, plane, L, vpad, vmax, mode, MP, st)
+#define OZ2_LE(R, C, A) launch_encode<R, C, A>(d.ptr, d.ld, d.contig, nvec, len, sft, out, plane, L, vpad, vmax, mode, flags, MP, st)
     if (d.dbl) {
         if (d.cplx) { if (is_A) OZ2_LE(double, true, true); else OZ2_LE(double, true, false); }
         else OZ2_LE(double, false, false);
@@ -441,8 +460,9 @@ void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, cons
 }
 
 void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
-                             hipStream_t st) {
-    finalize_accurate_sft_kernel<<<dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, st>>>(sft0, bound, nvec, log2M, out);
+                             hipStream_t st, bool cplx_rows) {
+    finalize_accurate_sft_kernel<<<dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, st>>>(sft0, bound, nvec, log2M, out,
+                                                                                          cplx_rows ? 1 : 0);
 }
 
 }  // namespace oz2

@@ -28,10 +28,10 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         p, sz, u, i, c = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int, ctypes.c_char
         _lib.oz2o_scaling.argtypes = [c, c, i, i, sz, sz, sz, p, sz, p, sz, u, i, i, p, p, p, p]
-        _lib.oz2o_scaling_ex.argtypes = [c, c, i, i, sz, sz, sz, p, sz, p, sz, u, i, i, p, p, p, p, p, p]
+        _lib.oz2o_scaling_ex.argtypes = [c, c, i, i, sz, sz, sz, p, sz, p, sz, u, i, i, p, p, p, p, p, p, i]
         _lib.oz2o_residues.argtypes = [sz, sz, sz, u, p, p, p]
         _lib.oz2o_crt.argtypes = [c, i, sz, sz, u, p, p, p, p, p, p, sz, i]
-        _lib.oz2o_gemm.argtypes = [c, c, c, i, i, sz, sz, sz, p, p, sz, p, sz, p, p, sz, u, i, i, i, p, p]
+        _lib.oz2o_gemm.argtypes = [c, c, c, i, i, sz, sz, sz, p, p, sz, p, sz, p, p, sz, u, i, i, i, p, p, i]
     return _lib
 
 
@@ -48,7 +48,7 @@ def default_vt(ta, tb):
     return 512 if (ta == np.float32 and tb == np.float32) else 128
 
 
-def scaling(A, B, num_moduli, fastmode=True, opA=0, opB=0, vt=None, colmax_in=None, want_colmax=False):
+def scaling(A, B, num_moduli, fastmode=True, opA=0, opB=0, vt=None, colmax_in=None, want_colmax=False, ctype=None):
     """Returns (A8 [N, mr, kr], B8 [N, n, kr], sftA [m], sftB [n]) for column-major A, B.
 
     Accurate mode only: colmax_in replaces the bound product's column maxima (row-block
@@ -69,7 +69,8 @@ def scaling(A, B, num_moduli, fastmode=True, opA=0, opB=0, vt=None, colmax_in=No
     cout = np.zeros(n, np.int32) if want_colmax else None
     rc = lib().oz2o_scaling_ex(tcode(A.dtype), tcode(B.dtype), opA, opB, m, n, k, _ptr(A), A.shape[0], _ptr(B),
                                B.shape[0], num_moduli, int(fastmode), vt, _ptr(A8), _ptr(B8), _ptr(sA), _ptr(sB),
-                               None if cin is None else _ptr(cin), None if cout is None else _ptr(cout))
+                               None if cin is None else _ptr(cin), None if cout is None else _ptr(cout),
+                               (1 if cp else 0) if ctype is None else ctype)
     if rc:
         raise ValueError(f"oz2o_scaling rc={rc}")
     return (A8, B8, sA, sB, cout) if want_colmax else (A8, B8, sA, sB)
@@ -98,7 +99,7 @@ def crt(R, sftA, sftB, out_dtype, alpha=1.0, beta=0.0, C=None, quirks=False):
 
 
 def gemm(A, B, num_moduli, fastmode=True, out_dtype=None, alpha=1.0, beta=0.0, C=None, opA=0, opB=0,
-         vt=None, quirks=False, return_sft=False):
+         vt=None, quirks=False, return_sft=False, ctype=None):
     """C = alpha * op(A) @ op(B) + beta * C through the restated reference pipeline."""
     A = np.asfortranarray(A)
     B = np.asfortranarray(B)
@@ -116,7 +117,7 @@ def gemm(A, B, num_moduli, fastmode=True, out_dtype=None, alpha=1.0, beta=0.0, C
     sB = np.zeros(n, np.int16)
     rc = lib().oz2o_gemm(tcode(A.dtype), tcode(B.dtype), tcode(out_dtype), opA, opB, m, n, k, _ptr(al), _ptr(A),
                          A.shape[0], _ptr(B), B.shape[0], _ptr(be), _ptr(C), C.shape[0], num_moduli, int(fastmode),
-                         vt, int(quirks), _ptr(sA), _ptr(sB))
+                         vt, int(quirks), _ptr(sA), _ptr(sB), 0 if ctype is None else ctype)
     if rc:
         raise ValueError(f"oz2o_gemm rc={rc}")
     return (C, sA, sB) if return_sft else C

@@ -116,6 +116,7 @@ typedef struct {
     char t;
     size_t ld;
     int contiguous; /* 1: vector elements are adjacent (A op T / B op N) */
+    int conj;       /* op C: the imaginary part enters negated */
 } vec_src;
 
 static void load(const vec_src *s, size_t v, size_t e, double *re, double *im) {
@@ -126,6 +127,7 @@ static void load(const vec_src *s, size_t v, size_t e, double *re, double *im) {
     case 'z': *re = ((const double *)s->base)[2 * idx]; *im = ((const double *)s->base)[2 * idx + 1]; break;
     default: *re = ((const float *)s->base)[2 * idx]; *im = ((const float *)s->base)[2 * idx + 1]; break;
     }
+    if (s->conj) *im = -*im;
 }
 
 /* ------------------------------------------------------------------ */
@@ -284,12 +286,34 @@ static void encode(double x, int dbl, int32_t sft, unsigned N, int8_t *out, size
 /* ------------------------------------------------------------------ */
 /* scaling stage                                                       */
 /* ------------------------------------------------------------------ */
+/* all N residue slices of vector v: real -> X8 row v; complex A -> big-matrix rows
+ * v = [re, -im] and v + nvec = [im, re] (scaling.hpp:753-838); complex B -> column
+ * [re; im] (:1150-1230).  op C arrives through vec_src.conj (:840-1089, 1232-1498). */
+static void encode_vector(const vec_src *s, size_t v, size_t k, unsigned N, int32_t sft, int is_A, int8_t *X8,
+                          size_t nvec, size_t kr, size_t inc) {
+    int dbl = is_dbl(s->t), cp = is_cplx(s->t);
+    for (size_t e = 0; e < k; ++e) {
+        double re, im;
+        load(s, v, e, &re, &im);
+        if (!cp) {
+            encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
+        } else if (is_A) {
+            encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
+            encode(im, dbl, sft, N, X8 + v * kr + k + e, inc, 1);
+            encode(im, dbl, sft, N, X8 + (v + nvec) * kr + e, inc, 0);
+            encode(re, dbl, sft, N, X8 + (v + nvec) * kr + k + e, inc, 0);
+        } else {
+            encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
+            encode(im, dbl, sft, N, X8 + v * kr + k + e, inc, 0);
+        }
+    }
+}
 /* Slices: X8[j*(nv*kr) + v*kr + e], kr = k (real) or 2k (complex big
  * matrix).  For complex A the big-matrix rows v and v+m are produced
  * (scaling.hpp:753-838), for complex B the column [re; im] (:1150-1230). */
 static void fast_vectors(const vec_src *s, size_t nvec, size_t k, unsigned N, int VT, float log2M,
                          int is_A, int8_t *X8, size_t nrows8, size_t kr, int16_t *sft_out) {
-    int dbl = is_dbl(s->t), cp = is_cplx(s->t);
+    int dbl = is_dbl(s->t);
     size_t inc = nrows8 * kr;
 #pragma omp parallel for schedule(dynamic, 4)
     for (size_t v = 0; v < nvec; ++v) {
@@ -304,27 +328,18 @@ static void fast_vectors(const vec_src *s, size_t nvec, size_t k, unsigned N, in
             sft = sft_fast_f(amax, nrm, log2M);
         }
         sft_out[v] = (int16_t)(uint16_t)(uint32_t)wrap32(-(int64_t)sft);
-        for (size_t e = 0; e < k; ++e) {
-            double re, im;
-            load(s, v, e, &re, &im);
-            if (!cp) {
-                encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
-            } else if (is_A) {
-                encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
-                encode(im, dbl, sft, N, X8 + v * kr + k + e, inc, 1);
-                encode(im, dbl, sft, N, X8 + (v + nvec) * kr + e, inc, 0);
-                encode(re, dbl, sft, N, X8 + (v + nvec) * kr + k + e, inc, 0);
-            } else {
-                encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
-                encode(im, dbl, sft, N, X8 + v * kr + k + e, inc, 0);
-            }
-        }
+        encode_vector(s, v, k, N, sft, is_A, X8, nvec, kr, inc);
     }
 }
 
-/* 6-bit magnitude extraction (extract_A8i_kernel / extract_B8i_kernel) */
-static void extract6(const vec_src *s, size_t nvec, size_t k, int8_t *X6, int16_t *sft0) {
-    int dbl = is_dbl(s->t);
+/* 6-bit magnitude extraction: sft0 = 5 - ilogb(amax), q = ceil(|x| * 2^sft0)
+ * (extract_A8i_kernel / extract_B8i_kernel, scaling.hpp:1897-1941, 2215-2260).  Complex
+ * (big matrix, op N): amax over max(|re|, |im|) (find_amax :115-153); A rows
+ * v = [qr, -qi], v + nvec = [qi, qr] (:1944-2016), B columns [qr; qi] (:2263-2329).
+ * X6 is [rows][kr] with kr = k (real) or 2k (complex). */
+static void extract6(const vec_src *s, size_t nvec, size_t k, int is_A, int btail, int8_t *X6, int16_t *sft0) {
+    int dbl = is_dbl(s->t), cp = is_cplx(s->t);
+    size_t kr = cp ? 2 * k : k;
 #pragma omp parallel for schedule(static)
     for (size_t v = 0; v < nvec; ++v) {
         double amax = 0.0;
@@ -333,31 +348,45 @@ static void extract6(const vec_src *s, size_t nvec, size_t k, int8_t *X6, int16_
             load(s, v, e, &re, &im);
             double a = dbl ? fabs(re) : (double)fabsf((float)re);
             if (a > amax) amax = a;
+            if (cp) {
+                double b = dbl ? fabs(im) : (double)fabsf((float)im);
+                if (b > amax) amax = b;
+            }
         }
         int32_t sf = dbl ? wrap32(5 - (int64_t)ilogb_d(amax)) : wrap32(5 - (int64_t)ilogb_f((float)amax));
         sft0[v] = (int16_t)sf;
         for (size_t e = 0; e < k; ++e) {
             double re, im;
             load(s, v, e, &re, &im);
-            int32_t q = dbl ? d2i_ru(scalbn_w(fabs(re), sf)) : d2i_ru((double)scalbnf_w(fabsf((float)re), sf));
-            X6[v * k + e] = (int8_t)(uint8_t)(uint32_t)q;
+            int32_t qr = dbl ? d2i_ru(scalbn_w(fabs(re), sf)) : d2i_ru((double)scalbnf_w(fabsf((float)re), sf));
+            int8_t br = (int8_t)(uint8_t)(uint32_t)qr;
+            X6[v * kr + e] = br;
+            if (cp) {
+                int32_t qi = dbl ? d2i_ru(scalbn_w(fabs(im), sf)) : d2i_ru((double)scalbnf_w(fabsf((float)im), sf));
+                int8_t bi = (int8_t)(uint8_t)(uint32_t)qi;
+                if (is_A) {
+                    X6[v * kr + k + e] = neg8(bi);
+                    X6[(v + nvec) * kr + e] = bi;
+                    X6[(v + nvec) * kr + k + e] = br;
+                } else {
+                    /* btail: big-matrix B, the reference's tail loop stores the last k mod 4
+                     * imaginary magnitudes outside the column (scaling.hpp:2313-2321) */
+                    X6[v * kr + k + e] = (btail && e >= (k & ~(size_t)3)) ? 0 : bi;
+                }
+            }
         }
     }
 }
 
 static void accurate_vectors(const vec_src *s, size_t nvec, size_t k, unsigned N, const int32_t *amax_bound,
-                             const int16_t *sft0, float log2M, int8_t *X8, size_t kr, int16_t *sft_out) {
-    int dbl = is_dbl(s->t);
-    size_t inc = nvec * kr;
+                             const int16_t *sft0, float log2M, int is_A, int8_t *X8, size_t nrows8, size_t kr,
+                             int16_t *sft_out) {
+    size_t inc = nrows8 * kr;
 #pragma omp parallel for schedule(dynamic, 4)
     for (size_t v = 0; v < nvec; ++v) {
         int32_t sft = sft_accu(amax_bound[v], sft0[v], log2M);
         sft_out[v] = (int16_t)(uint16_t)(uint32_t)wrap32(-(int64_t)sft);
-        for (size_t e = 0; e < k; ++e) {
-            double re, im;
-            load(s, v, e, &re, &im);
-            encode(re, dbl, sft, N, X8 + v * kr + e, inc, 0);
-        }
+        encode_vector(s, v, k, N, sft, is_A, X8, nvec, kr, inc);
     }
 }
 
@@ -367,18 +396,23 @@ static void accurate_vectors(const vec_src *s, size_t nvec, size_t k, unsigned N
 /* opA/opB: 0 = N, 1 = T.  VT: threads_scaling of the reference entry point
  * (gemmul8.cu:206-222 etc.: 128 for gemm<double>, mixed and complex, 512 for
  * gemm<float>).  Returns 0 on success. */
-/* colmax_out (optional): the bound product's column maxima of this call (accurate mode);
+/* ctype: compute type (0 real, 1 big matrix, 2 classic, 3 Karatsuba); the complex types share
+ * one computation except for the accurate-mode big-matrix B tail defect (extract6).
+ * colmax_out (optional): the bound product's column maxima of this call (accurate mode);
  * colmax_in (optional): column maxima to use instead (a row-block shard after the MAX
  * all-reduce over the other blocks, gemmul8/dist.py). */
 int oz2o_scaling_ex(char ta, char tb, int opA, int opB, size_t m, size_t n, size_t k, const void *A, size_t lda,
                     const void *B, size_t ldb, unsigned N, int fastmode, int VT, int8_t *A8, int8_t *B8,
-                    int16_t *sftA, int16_t *sftB, const int32_t *colmax_in, int32_t *colmax_out) {
+                    int16_t *sftA, int16_t *sftB, const int32_t *colmax_in, int32_t *colmax_out, int ctype) {
     if (N < 2 || N > 20) return -1;
     int cp = is_cplx(ta) || is_cplx(tb);
     if (cp && (!is_cplx(ta) || !is_cplx(tb))) return -2;
-    if (cp && (opA != 0 || opB != 0)) return -3;
-    vec_src sa = {A, ta, lda, opA != 0};
-    vec_src sb = {B, tb, ldb, opB == 0};
+    if (!cp && (opA == 2 || opB == 2)) { /* op C of a real operand is op T */
+        if (opA == 2) opA = 1;
+        if (opB == 2) opB = 1;
+    }
+    vec_src sa = {A, ta, lda, opA != 0, opA == 2};
+    vec_src sb = {B, tb, ldb, opB == 0, opB == 2};
     size_t kr = cp ? 2 * k : k;
     size_t mr = cp ? 2 * m : m;
     if (fastmode) {
@@ -387,40 +421,45 @@ int oz2o_scaling_ex(char ta, char tb, int opA, int opB, size_t m, size_t n, size
         fast_vectors(&sb, n, k, N, VT, log2M, 0, B8, n, kr, sftB);
         return 0;
     }
-    if (cp) return -4; /* complex accurate mode: not restated */
-    int8_t *A6 = (int8_t *)malloc(m * k), *B6 = (int8_t *)malloc(n * k);
+    if (cp && (opA != 0 || opB != 0)) return -3; /* complex accurate mode: op N only (restated) */
+    int8_t *A6 = (int8_t *)malloc(mr * kr), *B6 = (int8_t *)malloc(n * kr);
     int16_t *s0A = (int16_t *)malloc(m * 2), *s0B = (int16_t *)malloc(n * 2);
     int32_t *amA = (int32_t *)calloc(m, 4), *amB = (int32_t *)calloc(n, 4);
-    extract6(&sa, m, k, A6, s0A);
-    extract6(&sb, n, k, B6, s0B);
-    /* bound product C32 = A6 * B6^T, then row / column max of |C32| */
+    extract6(&sa, m, k, 1, 0, A6, s0A);
+    extract6(&sb, n, k, 0, cp && ctype == 1, B6, s0B);
+    /* bound product C32 = A6 * B6^T (mr x n), then row / column max of |C32|; complex: the
+     * row bound of v is max over rows v and v + m (scalingA_kernel_bigmatrix :2561-2588), the
+     * column bound over all 2m rows (scalingB_kernel_bigmatrix :2706-2732) */
+    int32_t *rowmax = (int32_t *)calloc(mr, 4);
 #pragma omp parallel for schedule(static)
-    for (size_t r = 0; r < m; ++r) {
+    for (size_t r = 0; r < mr; ++r) {
         int32_t mx = 0;
         for (size_t c = 0; c < n; ++c) {
             int32_t acc = 0;
-            for (size_t e = 0; e < k; ++e) acc += (int32_t)A6[r * k + e] * (int32_t)B6[c * k + e];
+            for (size_t e = 0; e < kr; ++e) acc += (int32_t)A6[r * kr + e] * (int32_t)B6[c * kr + e];
             int32_t a = acc < 0 ? -acc : acc;
             if (a > mx) mx = a;
         }
-        amA[r] = mx;
+        rowmax[r] = mx;
     }
+    for (size_t r = 0; r < m; ++r) amA[r] = cp ? (rowmax[r] > rowmax[r + m] ? rowmax[r] : rowmax[r + m]) : rowmax[r];
 #pragma omp parallel for schedule(static)
     for (size_t c = 0; c < n; ++c) {
         int32_t mx = 0;
-        for (size_t r = 0; r < m; ++r) {
+        for (size_t r = 0; r < mr; ++r) {
             int32_t acc = 0;
-            for (size_t e = 0; e < k; ++e) acc += (int32_t)A6[r * k + e] * (int32_t)B6[c * k + e];
+            for (size_t e = 0; e < kr; ++e) acc += (int32_t)A6[r * kr + e] * (int32_t)B6[c * kr + e];
             int32_t a = acc < 0 ? -acc : acc;
             if (a > mx) mx = a;
         }
         amB[c] = mx;
     }
+    free(rowmax);
     if (colmax_out) memcpy(colmax_out, amB, n * sizeof(int32_t));
     if (colmax_in) memcpy(amB, colmax_in, n * sizeof(int32_t));
     float log2M = oz2_log2M_accu[N - 2];
-    accurate_vectors(&sa, m, k, N, amA, s0A, log2M, A8, kr, sftA);
-    accurate_vectors(&sb, n, k, N, amB, s0B, log2M, B8, kr, sftB);
+    accurate_vectors(&sa, m, k, N, amA, s0A, log2M, 1, A8, mr, kr, sftA);
+    accurate_vectors(&sb, n, k, N, amB, s0B, log2M, 0, B8, n, kr, sftB);
     free(A6); free(B6); free(s0A); free(s0B); free(amA); free(amB);
     return 0;
 }
@@ -428,7 +467,8 @@ int oz2o_scaling_ex(char ta, char tb, int opA, int opB, size_t m, size_t n, size
 int oz2o_scaling(char ta, char tb, int opA, int opB, size_t m, size_t n, size_t k, const void *A, size_t lda,
                  const void *B, size_t ldb, unsigned N, int fastmode, int VT, int8_t *A8, int8_t *B8,
                  int16_t *sftA, int16_t *sftB) {
-    return oz2o_scaling_ex(ta, tb, opA, opB, m, n, k, A, lda, B, ldb, N, fastmode, VT, A8, B8, sftA, sftB, NULL, NULL);
+    return oz2o_scaling_ex(ta, tb, opA, opB, m, n, k, A, lda, B, ldb, N, fastmode, VT, A8, B8, sftA, sftB, NULL, NULL,
+                           is_cplx(ta) ? 1 : 0);
 }
 
 /* conv_32i_2_8u (conv_32i_2_8u.hpp:7-56) */
@@ -562,14 +602,15 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
  * (may be NULL).  complex_bm selects COMPLEX_BIG_MATRIX_ENCODE. */
 int oz2o_gemm(char ta, char tb, char tc, int opA, int opB, size_t m, size_t n, size_t k, const void *alpha,
               const void *A, size_t lda, const void *B, size_t ldb, const void *beta, void *C, size_t ldc,
-              unsigned N, int fastmode, int VT, int quirks, int16_t *sftA_out, int16_t *sftB_out) {
+              unsigned N, int fastmode, int VT, int quirks, int16_t *sftA_out, int16_t *sftB_out, int ctype) {
     int cp = is_cplx(ta);
     size_t kr = cp ? 2 * k : k, mr = cp ? 2 * m : m;
     int8_t *A8 = (int8_t *)malloc((size_t)N * mr * kr + 1);
     int8_t *B8 = (int8_t *)malloc((size_t)N * n * kr + 1);
     uint8_t *R = (uint8_t *)malloc((size_t)N * mr * n + 1);
     int16_t *sA = (int16_t *)malloc(m * 2 + 2), *sB = (int16_t *)malloc(n * 2 + 2);
-    int rc = oz2o_scaling(ta, tb, opA, opB, m, n, k, A, lda, B, ldb, N, fastmode, VT, A8, B8, sA, sB);
+    int rc = oz2o_scaling_ex(ta, tb, opA, opB, m, n, k, A, lda, B, ldb, N, fastmode, VT, A8, B8, sA, sB, NULL, NULL,
+                             cp ? (ctype ? ctype : 1) : 0);
     if (rc == 0) rc = oz2o_residues(mr, n, kr, N, A8, B8, R);
     if (rc == 0) rc = oz2o_crt(tc, cp, m, n, N, R, sA, sB, alpha, beta, C, ldc, quirks);
     if (sftA_out) memcpy(sftA_out, sA, m * 2);

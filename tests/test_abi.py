@@ -56,11 +56,12 @@ def test_work_size_and_errors_host_only():
     lib.gemmul8_gemm.argtypes = [p, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, p, p, ctypes.c_size_t, p, ctypes.c_size_t,
                                  p, p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int, p, ctypes.c_int, p]
-    args = lambda N, ta=0, tb=0, tc=0, ct=0, k=8: (None, 0, 0, 8, 8, k, ta, tb, tc, None, None, 8, None, k, None,
-                                                    None, 8, N, 1, None, ct, None)
+    args = lambda N, ta=0, tb=0, tc=0, ct=0, k=8, opa=0, fast=1: (None, opa, 0, 8, 8, k, ta, tb, tc, None, None, 8,
+                                                                  None, k, None, None, 8, N, fast, None, ct, None)
     assert lib.gemmul8_gemm(*args(1)) == -1
     assert lib.gemmul8_gemm(*args(21)) == -1
     assert lib.gemmul8_gemm(*args(14, ta=2)) == -2          # complex A with real B
     assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2)) == -2  # complex types need COMPLEX_BIG_MATRIX_ENCODE
-    assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2, ct=3)) == -5  # Karatsuba: not in this build
+    # complex accurate mode is restated for op N x op N only
+    assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2, ct=3, opa=1, fast=0)) == -5
     assert lib.gemmul8_gemm(*args(14, k=(1 << 17) + 1)) == -4

@@ -29,7 +29,7 @@ def to_dev(X):
     return torch.from_numpy(np.ascontiguousarray(Xf.T)).cuda()
 
 
-def run_gpu(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta=0.0, C0=None):
+def run_gpu(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta=0.0, C0=None, ctype=None):
     torch = _torch()
     import gemmul8 as G
     A = np.asfortranarray(A)
@@ -39,7 +39,7 @@ def run_gpu(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta=0.
     n = B.shape[0] if opB else B.shape[1]
     out_dtype = out_dtype or np.result_type(A.dtype, B.dtype)
     cplx = np.iscomplexobj(A)
-    ct = G.COMPLEX_BIG_MATRIX_ENCODE if cplx else G.REAL_DEFAULT
+    ct = (ctype or G.COMPLEX_BIG_MATRIX_ENCODE) if cplx else G.REAL_DEFAULT
     if C0 is None:
         C0 = np.zeros((m, n), out_dtype, order="F")
     dA, dB, dC = to_dev(A), to_dev(B), to_dev(np.asfortranarray(C0.astype(out_dtype)))
@@ -67,7 +67,7 @@ def ws_residues(wsb, L, N):
     return R
 
 
-def check_full(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta=0.0, C0=None, vt=None):
+def check_full(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta=0.0, C0=None, vt=None, ctype=None):
     from oracle import oracle as O
     A = np.asfortranarray(A)
     B = np.asfortranarray(B)
@@ -76,8 +76,8 @@ def check_full(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta
     n = B.shape[0] if opB else B.shape[1]
     cplx = np.iscomplexobj(A)
     out_dtype = out_dtype or np.result_type(A.dtype, B.dtype)
-    C, wsb, L = run_gpu(A, B, N, fast, opA, opB, out_dtype, alpha, beta, C0)
-    A8o, B8o, sAo, sBo = O.scaling(A, B, N, fast, opA, opB, vt)
+    C, wsb, L = run_gpu(A, B, N, fast, opA, opB, out_dtype, alpha, beta, C0, ctype)
+    A8o, B8o, sAo, sBo = O.scaling(A, B, N, fast, opA, opB, vt, ctype=ctype)
     sA, sB = ws_sft(wsb, L, m, n)
     agree_A = float(np.mean(sA == sAo)) if m else 1.0
     agree_B = float(np.mean(sB == sBo)) if n else 1.0
@@ -99,7 +99,7 @@ def check_full(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta
     Ro = O.residues(A8o, B8o)
     mr = 2 * m if cplx else m
     assert np.array_equal(R[:, :n, :mr], Ro), "residue mismatch"
-    Co = O.gemm(A, B, N, fast, out_dtype, alpha, beta, C0, opA, opB, vt)
+    Co = O.gemm(A, B, N, fast, out_dtype, alpha, beta, C0, opA, opB, vt, ctype=ctype)
     assert bits_equal(C, Co), f"C mismatch: max |diff| {np.max(np.abs(C - Co))}"
     return C, Co
 
@@ -176,6 +176,35 @@ def test_every_specialization(ta, tb, tc):
 def test_extreme_shapes(m, n, k, N):
     rng = np.random.default_rng(m + n + k)
     check_full(randmat_np(rng, m, k), randmat_np(rng, k, n), N)
+
+
+@pytest.mark.parametrize("opA,opB", [(1, 0), (2, 0), (0, 1), (0, 2), (1, 2), (2, 1), (2, 2)])
+def test_complex_ops(opA, opB):
+    """complex op T / op C on either side (big-matrix encode, fast mode; scaling.hpp:3736-3804)"""
+    rng = np.random.default_rng(31 + 3 * opA + opB)
+    m, n, k = 45, 38, 70
+    A = randmat_np(rng, k, m, dtype=np.complex128) if opA else randmat_np(rng, m, k, dtype=np.complex128)
+    B = randmat_np(rng, n, k, dtype=np.complex128) if opB else randmat_np(rng, k, n, dtype=np.complex128)
+    check_full(A, B, 12, opA=opA, opB=opB)
+    check_full(A.astype(np.complex64), B.astype(np.complex64), 7, opA=opA, opB=opB)
+
+
+@pytest.mark.parametrize("ctype", [1, 2, 3])
+@pytest.mark.parametrize("dt,N,k", [(np.complex128, 12, 45), (np.complex64, 7, 33), (np.complex128, 9, 64)])
+def test_complex_accurate(ctype, dt, N, k):
+    """complex accurate mode (op N), all three compute types; k mod 4 != 0 exercises the
+    big-matrix B tail defect the reference's shifts carry (scaling.hpp:2313-2321)"""
+    rng = np.random.default_rng(ctype * 100 + N + k)
+    A, B = randmat_np(rng, 50, k, dtype=dt), randmat_np(rng, k, 36, dtype=dt)
+    check_full(A, B, N, fast=False, ctype=ctype)
+
+
+@pytest.mark.parametrize("ctype", [2, 3])
+def test_classic_karatsuba_fast(ctype):
+    rng = np.random.default_rng(77 + ctype)
+    A, B = randmat_np(rng, 60, 50, dtype=np.complex128), randmat_np(rng, 50, 40, dtype=np.complex128)
+    check_full(A, B, 14, ctype=ctype, opA=0, opB=0)
+    check_full(A.astype(np.complex64), B, 8, ctype=ctype, out_dtype=np.complex128)
 
 
 def test_zero_rows_and_cols():

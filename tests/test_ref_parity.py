@@ -33,27 +33,32 @@ def _ref():
 CODES = {"d": 0, "s": 1, "z": 2, "c": 3}
 
 
+# (ta, tb, tc, m, n, k, num_moduli, fast, opA, opB, computeType)
 @pytest.mark.parametrize("case", [
-    ("d", "d", "d", 1024, 1024, 1024, 14, 1),
-    ("d", "d", "d", 1000, 700, 1500, 8, 1),
-    ("s", "s", "s", 1024, 768, 2048, 6, 1),
-    ("d", "s", "d", 2048, 1536, 1000, 10, 0),
-    ("d", "d", "d", 1536, 1024, 2048, 14, 0),
-    ("z", "z", "z", 512, 640, 384, 12, 1),
-    ("d", "d", "d", 8192, 8192, 8192, 14, 1),   # cfg2
-    ("s", "s", "s", 1024, 1024, 1024, 4, 1),     # cfg1 shape on the GPU
-    ("d", "s", "d", 8192, 8192, 8192, 10, 0),    # cfg4
-    ("z", "z", "z", 4096, 4096, 4096, 12, 1),    # cfg5
+    ("d", "d", "d", 1024, 1024, 1024, 14, 1, 0, 0, 0),
+    ("d", "d", "d", 1000, 700, 1500, 8, 1, 0, 0, 0),
+    ("s", "s", "s", 1024, 768, 2048, 6, 1, 0, 0, 0),
+    ("d", "s", "d", 2048, 1536, 1000, 10, 0, 0, 0, 0),
+    ("d", "d", "d", 1536, 1024, 2048, 14, 0, 0, 0, 0),
+    ("z", "z", "z", 512, 640, 384, 12, 1, 0, 0, 1),
+    ("z", "z", "z", 600, 500, 700, 12, 1, 2, 1, 1),    # complex op C x op T
+    ("z", "z", "z", 250, 300, 301, 12, 0, 0, 0, 1),    # complex accurate, k mod 4 = 1 (m = 256 hits a reference defect)
+    ("c", "c", "c", 512, 384, 500, 7, 0, 0, 0, 3),     # Karatsuba, accurate
+    ("c", "c", "c", 300, 256, 333, 6, 1, 1, 2, 2),     # classic, op T x op C
+    ("d", "d", "d", 8192, 8192, 8192, 14, 1, 0, 0, 0),   # cfg2
+    ("s", "s", "s", 1024, 1024, 1024, 4, 1, 0, 0, 0),     # cfg1 shape on the GPU
+    ("d", "s", "d", 8192, 8192, 8192, 10, 0, 0, 0, 0),    # cfg4
+    ("z", "z", "z", 4096, 4096, 4096, 12, 1, 0, 0, 1),    # cfg5
 ])
 def test_same_inputs_same_bits(case):
     import torch
     import gemmul8 as G
-    ta, tb, tc, m, n, k, N, fast = case
+    ta, tb, tc, m, n, k, N, fast, opA, opB, ct = case
     lib = _ref()
     tdt = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}
-    A = G.randmat(m, k, tdt[ta], 0.5, 123456)
-    B = G.randmat(k, n, tdt[tb], 0.5, 123456)
-    ct = 1 if tc in "zc" else 0
+    A = G.randmat(k, m, tdt[ta], 0.5, 123456) if opA else G.randmat(m, k, tdt[ta], 0.5, 123456)
+    B = G.randmat(n, k, tdt[tb], 0.5, 654321) if opB else G.randmat(k, n, tdt[tb], 0.5, 123456)
+    lda, ldb = (k if opA else m), (n if opB else k)
     C_ref = torch.zeros((n, m), dtype=tdt[tc], device="cuda")
     C_new = torch.zeros_like(C_ref)
     npt = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}[tc]
@@ -63,12 +68,12 @@ def test_same_inputs_same_bits(case):
     wnew = G.alloc_work(m, n, k, N, ct)
 
     def run_ref():
-        rc = lib.ref_gemm(CODES[ta], CODES[tb], CODES[tc], 0, 0, m, n, k, one.ctypes.data, A.data_ptr(), m,
-                          B.data_ptr(), k, zero.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
+        rc = lib.ref_gemm(CODES[ta], CODES[tb], CODES[tc], opA, opB, m, n, k, one.ctypes.data, A.data_ptr(), lda,
+                          B.data_ptr(), ldb, zero.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
         assert rc == 0
 
     def run_new():
-        G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C_new, m, N, bool(fast), wnew, ct)
+        G.gemm(opA, opB, m, n, k, 1.0, A, lda, B, ldb, 0.0, C_new, m, N, bool(fast), wnew, ct)
 
     run_ref()
     run_new()
@@ -87,7 +92,8 @@ def test_same_inputs_same_bits(case):
             ts.append(time.perf_counter() - t0)
         tt[name] = float(np.median(ts))
     mult = 8 if ct else 2
-    RESULTS["%s%s%s_%dx%dx%d_N%d_%s" % (ta, tb, tc, m, n, k, N, "fast" if fast else "accu")] = {
+    RESULTS["%s%s%s_%dx%dx%d_N%d_%s_op%d%d_ct%d" % (ta, tb, tc, m, n, k, N, "fast" if fast else "accu", opA, opB,
+                                                   ct)] = {
         "bit_identical": bool(nbad == 0), "n_diff": nbad,
         "ref_ms": tt["reference"] * 1e3, "mi355x_ms": tt["mi355x"] * 1e3,
         "ref_tflops": mult * m * n * k / tt["reference"] / 1e12, "mi355x_tflops": mult * m * n * k / tt["mi355x"] / 1e12}
