@@ -65,3 +65,17 @@ def test_work_size_and_errors_host_only():
     # complex accurate mode is restated for op N x op N only
     assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2, ct=3, opa=1, fast=0)) == -5
     assert lib.gemmul8_gemm(*args(14, k=(1 << 17) + 1)) == -4
+
+
+def test_interposer_exports_and_has_no_runtime_dependency():
+    """libgemmul8_hijack.so: the intercepted hipBLAS / rocBLAS GEMM symbols, and no link-time HIP
+    or BLAS dependency (a second HIP runtime in a framework process would break it)."""
+    import subprocess
+    so = os.path.join(os.path.dirname(LIB), "libgemmul8_hijack.so")
+    assert os.path.exists(so)
+    syms = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True).stdout
+    for s in ("hipblasDgemm", "hipblasZgemm", "hipblasSgemm", "hipblasCgemm", "hipblasDgemmStridedBatched",
+              "hipblasZgemmStridedBatched", "rocblas_dgemm", "rocblas_zgemm", "rocblas_sgemm", "rocblas_cgemm"):
+        assert f" T {s}\n" in syms, s
+    needed = subprocess.run(["readelf", "-d", so], capture_output=True, text=True).stdout
+    assert "amdhip64" not in needed and "hipblas" not in needed and "rocblas" not in needed

@@ -1,0 +1,56 @@
+"""GPU: the hipBLAS/rocBLAS GEMM interposer (mixed-gemmul8_amd/csrc/hijack.cpp) under an unmodified
+PyTorch.  A child process loads libgemmul8_hijack.so into the global symbol scope before torch
+(the in-process equivalent of LD_PRELOAD), then calls torch.matmul: float64 / complex128
+products at or above the intercept thresholds must be the emulator's result bit for bit, smaller
+ones must reach the vendor routine."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HIJACK = os.path.join(ROOT, "mixed-gemmul8_amd", "gemmul8", "libgemmul8_hijack.so")
+
+CHILD = r'''
+import ctypes, json, sys
+ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)
+import torch
+sys.path.insert(0, sys.argv[2])
+import gemmul8 as G
+out = {}
+g = torch.Generator(device="cuda").manual_seed(5)
+for name, dt, (m, k, n) in (("d", torch.float64, (512, 448, 384)), ("z", torch.complex128, (300, 260, 280))):
+    A = torch.randn(m, k, dtype=dt, device="cuda", generator=g)
+    B = torch.randn(k, n, dtype=dt, device="cuda", generator=g)
+    C = torch.matmul(A, B)                       # torch -> hipblas{D,Z}gemm -> interposer
+    # torch multiplies column-major: C^T = B^T A^T, so the emulated "A" operand is B^T
+    E = G.matmul(B.t().contiguous(), A.t().contiguous(), 14).t()
+    exact = (A.cpu().to(torch.complex128) @ B.cpu().to(torch.complex128))
+    out[name] = {"bits": bool(torch.equal(C, E)),
+                 "relerr": float(((C.cpu().to(torch.complex128) - exact).abs() / exact.abs()).max())}
+A = torch.randn(64, 64, dtype=torch.float64, device="cuda", generator=g)
+C = A @ A                                        # below the thresholds: forwarded
+out["small_relerr"] = float(((C - (A.cpu() @ A.cpu()).cuda()).abs().max() / (A.cpu() @ A.cpu()).abs().max()))
+print("RESULT " + json.dumps(out))
+'''
+
+
+def test_torch_matmul_is_emulated():
+    assert os.path.exists(HIJACK), "libgemmul8_hijack.so not built"
+    env = dict(os.environ, GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14")
+    r = subprocess.run([sys.executable, "-c", CHILD, HIJACK, os.path.join(ROOT, "mixed-gemmul8_amd")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1]
+    res = json.loads(line[len("RESULT "):])
+    log = r.stderr
+    assert "[gemmul8] hipblasDgemm m=384 n=512 k=448 -> emulated" in log, log[-2000:]
+    assert "[gemmul8] hipblasZgemm m=280 n=300 k=260 -> emulated" in log, log[-2000:]
+    assert "m=64 n=64" not in log  # below the intercept thresholds: never reaches the emulator
+    assert res["d"]["bits"] and res["z"]["bits"], res
+    assert res["d"]["relerr"] < 1e-9 and res["z"]["relerr"] < 1e-9, res
+    assert res["small_relerr"] < 1e-12, res
