@@ -46,6 +46,18 @@ int gemmul8_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k,
                  const void *alpha, const void *A, size_t lda, const void *B, size_t ldb, const void *beta, void *C,
                  size_t ldc, unsigned num_moduli, int fastmode, void *work, int compute_type, double *phase_ns);
 
+/* --- low-memory mode ------------------------------------------------------
+ * The same product with only `slice_planes` planes of A / B slices resident: the moduli are
+ * encoded and multiplied in groups of that size (A and B are re-read once per group).  The
+ * result is bit-identical to gemmul8_gemm.  At 8192^3 with 14 moduli the workspace drops from
+ * 2.63 GiB to 1.13 GiB with slice_planes = 2.  slice_planes = 0 or >= num_moduli: all resident. */
+size_t gemmul8_work_size_lowmem(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type,
+                                unsigned slice_planes);
+int gemmul8_gemm_lowmem(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *alpha, const void *A, size_t lda, const void *B, size_t ldb,
+                        const void *beta, void *C, size_t ldc, unsigned num_moduli, int fastmode, void *work,
+                        int compute_type, unsigned slice_planes, double *phase_ns);
+
 /* --- phase entry points (multi-GPU sharding, gemmul8/dist.py) ------------------------------------
  * gemmul8_gemm == gemmul8_split(0, N) + gemmul8_products(0, N) + gemmul8_recombine, on one stream.
  * Splitting the moduli range lets rank r of a modulus-sharded job produce only the residue planes

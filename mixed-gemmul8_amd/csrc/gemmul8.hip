@@ -21,6 +21,7 @@ namespace oz2 {
 struct Call {
     OperandDesc A, B;
     int ctype;
+    unsigned slice_planes;  // 0: all N resident
     size_t m, n, k;
     unsigned N;
     bool fast;
@@ -85,9 +86,9 @@ struct Views {
     int16_t *sftA, *sftB, *sft0;
     int32_t *bound;
 };
-static Views views(void *work, size_t m, size_t n, size_t k, unsigned N, bool cplx) {
+static Views views(void *work, size_t m, size_t n, size_t k, unsigned N, bool cplx, unsigned slice_planes = 0) {
     Views v;
-    v.L = make_layout(m, n, k, N, cplx);
+    v.L = make_layout(m, n, k, N, cplx, slice_planes);
     int8_t *base = static_cast<int8_t *>(work);
     v.A8 = base + v.L.offA;
     v.B8 = base + v.L.offB;
@@ -128,11 +129,10 @@ static void phase_bound(const Call &c, const Views &v) {
     gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
 }
 
-// phase 1: shifts of every row of op(A) / column of op(B) (all moduli share them) and the
-// slices of moduli [j0, j1) (scaling.hpp:3680-3734 fast, :3053-3136 accurate).  bound_ready:
-// accurate mode takes the row / column maxima already in the workspace (phase_bound, possibly
-// combined across row blocks by the caller).
-static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1, bool bound_ready) {
+// phase 1a: shifts of every row of op(A) / column of op(B), shared by all moduli
+// (scaling.hpp:3680-3734 fast, :3053-3136 accurate).  bound_ready: accurate mode takes the row /
+// column maxima already in the workspace (phase_bound, possibly combined across row blocks).
+static void phase_shifts(const Call &c, const Views &v, bool bound_ready) {
     const Layout &L = v.L;
     if (c.fast) {
         const float log2M = oz2_log2M_fast[c.N - 2];
@@ -144,15 +144,26 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
         split_finalize_accurate(v.sft0, v.bound, c.m, log2M, v.sftA, c.st, c.cplx);
         split_finalize_accurate(v.sft0 + L.m_pad, v.bound + L.m_pad, c.n, log2M, v.sftB, c.st);
     }
-    const ModParams SP = sub_mod_params(c.N, j0, j1);
-    split_encode(c.A, true, c.m, c.k, v.sftA, v.A8 + j0 * L.planeA, L.planeA, L, 0, SP, c.st);
-    split_encode(c.B, false, c.n, c.k, v.sftB, v.B8 + j0 * L.planeB, L.planeB, L, 0, SP, c.st);
 }
 
-// phase 2: residue planes j0..j1-1 (one launch; conv_32i_2_8u fused into the epilogue)
-static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1, hipStream_t st) {
+// phase 1b: slices of moduli [j0, j1) into the slice planes starting at `slot`
+static void phase_encode(const Call &c, const Views &v, unsigned j0, unsigned j1, unsigned slot) {
     const Layout &L = v.L;
-    gemm_i8(v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB, L, j1 - j0, Epi::RESIDUE, v.R + j0 * L.planeR, nullptr,
+    const ModParams SP = sub_mod_params(c.N, j0, j1);
+    split_encode(c.A, true, c.m, c.k, v.sftA, v.A8 + slot * L.planeA, L.planeA, L, 0, SP, c.st);
+    split_encode(c.B, false, c.n, c.k, v.sftB, v.B8 + slot * L.planeB, L.planeB, L, 0, SP, c.st);
+}
+
+static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1, bool bound_ready) {
+    phase_shifts(c, v, bound_ready);
+    phase_encode(c, v, j0, j1, j0);
+}
+
+// phase 2: residue planes j0..j1-1 from the slice planes starting at `slot` (one launch;
+// conv_32i_2_8u fused into the epilogue)
+static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1, unsigned slot, hipStream_t st) {
+    const Layout &L = v.L;
+    gemm_i8(v.A8 + slot * L.planeA, v.B8 + slot * L.planeB, L, j1 - j0, Epi::RESIDUE, v.R + j0 * L.planeR, nullptr,
             nullptr, sub_mod_params(N, j0, j1), st);
 }
 
@@ -164,7 +175,7 @@ static void phase_crt(const Views &v, unsigned N, OutType ot, const void *alpha,
 }
 
 static int run(const Call &c, double *phase_ns) {
-    const Views v = views(c.work, c.m, c.n, c.k, c.N, c.cplx);
+    const Views v = views(c.work, c.m, c.n, c.k, c.N, c.cplx, c.slice_planes);
 
     const bool want_events = phase_ns != nullptr;
     bool record;
@@ -176,10 +187,22 @@ static int run(const Call &c, double *phase_ns) {
     }
     if (record) (void)hipEventRecord(rec.start, c.st);
 
-    phase_split(c, v, 0, c.N, false);
-    if (record) (void)hipEventRecord(rec.ev[0], c.st);
-
-    phase_products(v, c.N, 0, c.N, c.st);
+    const unsigned S = v.L.S;
+    if (S >= c.N) {
+        phase_split(c, v, 0, c.N, false);
+        if (record) (void)hipEventRecord(rec.ev[0], c.st);
+        phase_products(v, c.N, 0, c.N, 0, c.st);
+    } else {
+        // low-memory mode: the moduli in groups of S through the same S slice planes (each group
+        // re-reads A and B); the product phase timer then includes the re-encoding
+        phase_shifts(c, v, false);
+        if (record) (void)hipEventRecord(rec.ev[0], c.st);
+        for (unsigned j0 = 0; j0 < c.N; j0 += S) {
+            const unsigned j1 = j0 + S < c.N ? j0 + S : c.N;
+            phase_encode(c, v, j0, j1, 0);
+            phase_products(v, c.N, j0, j1, 0, c.st);
+        }
+    }
     if (record) {
         (void)hipEventRecord(rec.ev[1], c.st);
         (void)hipEventRecord(rec.ev[2], c.st);
@@ -271,6 +294,25 @@ int gemmul8_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k,
     return oz2::run(c, phase_ns);
 }
 
+size_t gemmul8_work_size_lowmem(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type,
+                                unsigned slice_planes) {
+    if (compute_type < 0 || compute_type > 3) return 0;
+    return oz2::make_layout(m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT, slice_planes).total;
+}
+
+int gemmul8_gemm_lowmem(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *alpha, const void *A, size_t lda, const void *B, size_t ldb,
+                        const void *beta, void *C, size_t ldc, unsigned num_moduli, int fastmode, void *work,
+                        int compute_type, unsigned slice_planes, double *phase_ns) {
+    oz2::Call c{};
+    const int rc = oz2::prepare(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, alpha, A, lda, B, ldb, beta, C,
+                                ldc, num_moduli, fastmode, work, compute_type, c);
+    if (rc != GEMMUL8_OK) return rc;
+    c.slice_planes = slice_planes;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    return oz2::run(c, phase_ns);
+}
+
 int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
                         int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
                         void *work, int compute_type) {
@@ -321,7 +363,7 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
         (void)hipEventRecord(rec.start, st);
         (void)hipEventRecord(rec.ev[0], st);
     }
-    oz2::phase_products(v, num_moduli, mod_begin, mod_end, st);
+    oz2::phase_products(v, num_moduli, mod_begin, mod_end, mod_begin, st);
     if (record) {
         (void)hipEventRecord(rec.ev[1], st);
         (void)hipEventRecord(rec.ev[2], st);

@@ -46,14 +46,19 @@ struct Layout {
     size_t m_pad, n_pad, k_pad;
     size_t ksteps, mtiles, ntiles;
     size_t planeA, planeB, planeR;  // bytes per modulus
+    unsigned S;                     // slice planes held at once (= N unless low-memory mode)
     // workspace offsets (bytes)
     size_t offA, offB, offR, offSftA, offSftB, offBound, offSft0, total;
 };
 
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool cplx) {
+// slice_planes: planes of A / B slices held at once (N: all resident; fewer: the low-memory
+// mode encodes the moduli in groups of that size into the same planes, gemmul8.hip run())
+static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool cplx, unsigned slice_planes = 0) {
     Layout L{};
+    const unsigned S = (slice_planes == 0 || slice_planes > N) ? N : slice_planes;
+    L.S = S;
     L.m = m; L.n = n; L.k = k; L.N = N; L.cplx = cplx;
     L.kblk = round_up(k, KSTEP);
     L.mr = cplx ? 2 * m : m;
@@ -68,8 +73,8 @@ static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool 
     L.planeB = L.n_pad * L.k_pad;
     L.planeR = L.m_pad * L.n_pad;
     size_t off = 0;
-    L.offA = off; off += round_up(L.planeA * N, 256);
-    L.offB = off; off += round_up(L.planeB * N, 256);
+    L.offA = off; off += round_up(L.planeA * S, 256);
+    L.offB = off; off += round_up(L.planeB * S, 256);
     L.offR = off; off += round_up(L.planeR * N, 256);
     L.offSftA = off; off += round_up(L.m_pad * 2, 256);
     L.offSftB = off; off += round_up(L.n_pad * 2, 256);

@@ -44,6 +44,10 @@ def _load():
     lib.gemmul8_split_bound.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, sz, p, sz, u, p, i]
     lib.gemmul8_products.argtypes = [p, sz, sz, sz, u, i, p, u, u]
     lib.gemmul8_recombine.argtypes = [p, sz, sz, sz, u, i, i, p, p, p, sz, p]
+    lib.gemmul8_work_size_lowmem.restype = sz
+    lib.gemmul8_work_size_lowmem.argtypes = [sz, sz, sz, u, i, u]
+    lib.gemmul8_gemm_lowmem.restype = i
+    lib.gemmul8_gemm_lowmem.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, p, sz, p, sz, p, p, sz, u, i, p, i, u, d]
     lib.gemmul8_timing_enable.argtypes = [i]
     lib.gemmul8_timing_read.argtypes = [d, ctypes.POINTER(ctypes.c_int)]
     lib.gemmul8_layout.argtypes = [sz, sz, sz, u, i, ctypes.POINTER(ctypes.c_size_t)]
@@ -76,8 +80,10 @@ def _scalar(x, dtype):
     return np.array([x], dtype=npt)
 
 
-def workSize(m, n, k, num_moduli, computeType=REAL_DEFAULT):
-    """Bytes of device workspace for gemm (gemmul8.hpp:18-22)."""
+def workSize(m, n, k, num_moduli, computeType=REAL_DEFAULT, slice_planes=None):
+    """Bytes of device workspace for gemm (gemmul8.hpp:18-22); slice_planes: low-memory mode."""
+    if slice_planes:
+        return int(lib.gemmul8_work_size_lowmem(m, n, k, num_moduli, computeType, slice_planes))
     return int(lib.gemmul8_work_size(m, n, k, num_moduli, computeType))
 
 
@@ -90,7 +96,7 @@ def layout(m, n, k, num_moduli, computeType=REAL_DEFAULT):
 
 
 def gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fastmode, work,
-         computeType=REAL_DEFAULT, stream=None, phase_times=False):
+         computeType=REAL_DEFAULT, stream=None, phase_times=False, slice_planes=None):
     """C = alpha*op(A)*op(B) + beta*C on column-major device buffers (gemmul8.hpp:29-47).
 
     A, B, C, work: torch tensors (storage in column-major order, ld in elements).
@@ -99,9 +105,14 @@ def gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fas
     ta, tb, tc = _DTYPE[A.dtype], _DTYPE[B.dtype], _DTYPE[C.dtype]
     al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
     pt = (ctypes.c_double * 4)() if phase_times else None
-    rc = lib.gemmul8_gemm(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ctypes.data, A.data_ptr(), lda,
-                          B.data_ptr(), ldb, be.ctypes.data, C.data_ptr(), ldc, num_moduli, int(bool(fastmode)),
-                          work.data_ptr(), computeType, pt)
+    if slice_planes:
+        rc = lib.gemmul8_gemm_lowmem(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ctypes.data, A.data_ptr(),
+                                     lda, B.data_ptr(), ldb, be.ctypes.data, C.data_ptr(), ldc, num_moduli,
+                                     int(bool(fastmode)), work.data_ptr(), computeType, slice_planes, pt)
+    else:
+        rc = lib.gemmul8_gemm(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ctypes.data, A.data_ptr(), lda,
+                              B.data_ptr(), ldb, be.ctypes.data, C.data_ptr(), ldc, num_moduli, int(bool(fastmode)),
+                              work.data_ptr(), computeType, pt)
     _check(rc)
     return list(pt) if phase_times else None
 
@@ -154,8 +165,8 @@ def residue_planes(work, m, n, k, num_moduli, mod_begin=0, mod_end=None, compute
     return work[start:start + (mod_end - mod_begin) * L["planeR"]].view(mod_end - mod_begin, L["planeR"])
 
 
-def alloc_work(m, n, k, num_moduli, computeType=REAL_DEFAULT, device="cuda"):
-    return torch.empty(workSize(m, n, k, num_moduli, computeType), dtype=torch.uint8, device=device)
+def alloc_work(m, n, k, num_moduli, computeType=REAL_DEFAULT, device="cuda", slice_planes=None):
+    return torch.empty(workSize(m, n, k, num_moduli, computeType, slice_planes), dtype=torch.uint8, device=device)
 
 
 def matmul(A, B, num_moduli=14, fastmode=True, out_dtype=None, work=None):

@@ -136,3 +136,37 @@ def test_moduli_shards_assembled_on_root():
     out = ops.finish(root_st)
     torch.cuda.synchronize()
     assert _same(out, ref)
+
+
+@pytest.mark.parametrize("S", [1, 3, 13])
+@pytest.mark.parametrize("fast", [True, False])
+def test_low_memory_mode_same_bits(S, fast):
+    """gemmul8_gemm_lowmem: the moduli in groups of S through S slice planes"""
+    import torch
+    import gemmul8 as G
+    m, n, k, N = 300, 280, 333, 14
+    A, B = _rand(m, k, 11, torch.float64), _rand(k, n, 12, torch.float64)
+    ref = _single(A, B, N, fast, torch.float64)
+    assert G.workSize(m, n, k, N, slice_planes=S) < G.workSize(m, n, k, N)
+    work = G.alloc_work(m, n, k, N, slice_planes=S)
+    Ct = torch.empty((n, m), dtype=torch.float64, device="cuda")
+    G.gemm(G.OP_T, G.OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, N, fast, work, slice_planes=S)
+    torch.cuda.synchronize()
+    assert _same(Ct.t(), ref)
+
+
+def test_low_memory_mode_complex():
+    import torch
+    import gemmul8 as G
+    m, n, k, N = 200, 150, 170, 12
+    A, B = _rand(m, k, 13, torch.complex128), _rand(k, n, 14, torch.complex128)
+    Acm, Bcm = A.t().contiguous(), B.t().contiguous()
+    out = []
+    for S in (None, 5):
+        work = G.alloc_work(m, n, k, N, G.COMPLEX_BIG_MATRIX_ENCODE, slice_planes=S)
+        Ct = torch.empty((n, m), dtype=torch.complex128, device="cuda")
+        G.gemm(0, 0, m, n, k, 1.0, Acm, m, Bcm, k, 0.0, Ct, m, N, True, work, G.COMPLEX_BIG_MATRIX_ENCODE,
+               slice_planes=S)
+        out.append(Ct)
+    torch.cuda.synchronize()
+    assert _same(out[0], out[1])
