@@ -24,14 +24,18 @@ __global__ void rate_kernel(const int8_t *src, size_t span, int iters, long long
     const int8_t *base = src + (span == 65536 ? 0 : (size_t)blockIdx.x * span);
     long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
     v4i acc = {0, 0, 0, 0};
+#pragma unroll 8
     for (int it = 0; it < iters; ++it) {
         const size_t off = ((size_t)(it * nw + wave) * 1024) % span;
         if (MODE == 0) {
             glds16(base + off + lane * 16, lds + ((it * nw + wave) % 128) * 1024);
             __builtin_amdgcn_s_waitcnt((INFLIGHT & 15) | (7 << 4) | (15 << 8) | ((INFLIGHT >> 4) << 14));
-        } else {
+        } else if (MODE == 1) {
             v4i x = *reinterpret_cast<const v4i *>(base + off + lane * 16);
             acc ^= x;
+        } else {  // register staging: global_load_dwordx4 + ds_write_b128
+            v4i x = *reinterpret_cast<const v4i *>(base + off + lane * 16);
+            *reinterpret_cast<v4i *>(smem + ((it * nw + wave) % 128) * 1024 + lane * 16) = x;
         }
     }
     __builtin_amdgcn_s_waitcnt(0);
@@ -63,7 +67,8 @@ int main(int argc, char **argv) {
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
         if (mode == 0) rate_kernel<0, 8><<<blocks, threads>>>(src, span, iters, clk, sink);
-        else rate_kernel<1, 8><<<blocks, threads>>>(src, span, iters, clk, sink);
+        else if (mode == 1) rate_kernel<1, 8><<<blocks, threads>>>(src, span, iters, clk, sink);
+        else rate_kernel<2, 8><<<blocks, threads>>>(src, span, iters, clk, sink);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         float ms;
@@ -75,7 +80,7 @@ int main(int argc, char **argv) {
         cyc /= blocks; rt /= blocks;
         const double bytes = (double)iters * (threads / 64) * 1024;
         printf("mode=%s threads=%d src=%s: %.3f ms, %.1f B/clk/CU, clock %.2f GHz, %.1f GB/s/CU\n",
-               mode ? "vgpr" : "lds-dma", threads, l2 ? "l2" : "stream", ms, bytes / cyc, cyc / rt * 0.1,
+               mode == 2 ? "vgpr+ds_write" : mode ? "vgpr" : "lds-dma", threads, l2 ? "l2" : "stream", ms, bytes / cyc, cyc / rt * 0.1,
                bytes / (ms * 1e-3) / 1e9);
     }
     return 0;
