@@ -123,8 +123,9 @@ static void phase_bound(const Call &c, const Views &v) {
     split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.st);
     split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
     // big-matrix B magnitudes carry the reference's tail defect; classic / Karatsuba do not
+    // the B tail defect lives in the op-N big-matrix extraction only (scaling.hpp:2312-2323, 3201-3203)
     split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.st,
-                 c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE);
+                 c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE && c.B.contig);
     (void)hipMemsetAsync(v.bound, 0, (L.m_pad + L.n_pad) * sizeof(int32_t), c.st);
     gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
 }
@@ -251,8 +252,6 @@ static int prepare(void *stream, int op_a, int op_b, size_t m, size_t n, size_t 
     // output precision is the higher of the inputs' in every reference specialization (gemmul8.hpp:49-287)
     if (!cp && !(tc == GEMMUL8_R_64F || tc == GEMMUL8_R_32F)) return GEMMUL8_E_TYPES;
     if (op_a < 0 || op_a > 2 || op_b < 0 || op_b > 2) return GEMMUL8_E_OP;
-    // complex accurate mode is restated for op N x op N (scaling.hpp:3138-3245, 3247-3368)
-    if (cp && !fast && (op_a != GEMMUL8_OP_N || op_b != GEMMUL8_OP_N)) return GEMMUL8_E_UNSUPPORTED;
     const size_t kr = cp ? 2 * round_up(k, KSTEP) : round_up(k, KSTEP);
     if (kr > ((size_t)1 << 17)) return GEMMUL8_E_SIZE;
     const bool ta_t = op_a != GEMMUL8_OP_N, tb_t = op_b != GEMMUL8_OP_N;

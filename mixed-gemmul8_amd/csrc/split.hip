@@ -323,6 +323,10 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                 if (CPLX) {
                     int vi = std::is_same<R, double>::value ? __double2int_ru((double)yi[q]) : __float2int_ru((float)yi[q]);
                     if (kk + q >= tail) vi = 0;
+                    // op C: the reference's conjugate extractions carry the imaginary magnitude with the
+                    // opposite sign (A rows [qr, qi] / [-qi, qr], B columns [qr; -qi]:
+                    // scaling.hpp:2262-2329 with addCol, 1944-2016 without)
+                    if (flags & ENC_CONJ) vi = -vi;
                     ai |= ((uint32_t)vi & 0xffu) << (8 * b);
                 }
             }

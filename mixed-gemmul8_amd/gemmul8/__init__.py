@@ -186,7 +186,8 @@ def matmul(A, B, num_moduli=14, fastmode=True, out_dtype=None, work=None):
     if work is None:
         work = alloc_work(m, n, k, num_moduli, ct, A.device)
     if cplx:
-        # complex big-matrix encode supports op N only: materialise column-major operands
+        # complex: materialise column-major operands so the call is op N x op N, the form a BLAS
+        # caller (and the interposer) passes for a row-major product; its bits then match it
         Acm = A.t().contiguous()
         Bcm = B.t().contiguous()
         gemm(OP_N, OP_N, m, n, k, 1.0, Acm, m, Bcm, k, 0.0, Ct, m, num_moduli, fastmode, work, ct)

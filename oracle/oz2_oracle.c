@@ -364,6 +364,11 @@ static void extract6(const vec_src *s, size_t nvec, size_t k, int is_A, int btai
             if (cp) {
                 int32_t qi = dbl ? d2i_ru(scalbn_w(fabs(im), sf)) : d2i_ru((double)scalbnf_w(fabsf((float)im), sf));
                 int8_t bi = (int8_t)(uint8_t)(uint32_t)qi;
+                /* op C: the conjugate extractions carry the imaginary magnitude with the opposite
+                 * sign, A rows [qr, qi] / [-qi, qr] (extract_B8i_kernel_bigmatrix with addCol,
+                 * scaling.hpp:2262-2329), B columns [qr; -qi] (extract_A8i_kernel_bigmatrix without
+                 * addCol, :1944-2016); op T keeps the op-N signs (:2082-2149, 2395-2468) */
+                if (s->conj) bi = neg8(bi);
                 if (is_A) {
                     X6[v * kr + k + e] = neg8(bi);
                     X6[(v + nvec) * kr + e] = bi;
@@ -421,12 +426,12 @@ int oz2o_scaling_ex(char ta, char tb, int opA, int opB, size_t m, size_t n, size
         fast_vectors(&sb, n, k, N, VT, log2M, 0, B8, n, kr, sftB);
         return 0;
     }
-    if (cp && (opA != 0 || opB != 0)) return -3; /* complex accurate mode: op N only (restated) */
     int8_t *A6 = (int8_t *)malloc(mr * kr), *B6 = (int8_t *)malloc(n * kr);
     int16_t *s0A = (int16_t *)malloc(m * 2), *s0B = (int16_t *)malloc(n * 2);
     int32_t *amA = (int32_t *)calloc(m, 4), *amB = (int32_t *)calloc(n, 4);
     extract6(&sa, m, k, 1, 0, A6, s0A);
-    extract6(&sb, n, k, 0, cp && ctype == 1, B6, s0B);
+    /* the B tail defect lives in the op-N big-matrix extraction only (scaling.hpp:2312-2323) */
+    extract6(&sb, n, k, 0, cp && ctype == 1 && opB == 0, B6, s0B);
     /* bound product C32 = A6 * B6^T (mr x n), then row / column max of |C32|; complex: the
      * row bound of v is max over rows v and v + m (scalingA_kernel_bigmatrix :2561-2588), the
      * column bound over all 2m rows (scalingB_kernel_bigmatrix :2706-2732) */

@@ -60,6 +60,15 @@ def cases():
         out.append((f"ccc_ct{ctype}_accu_op00", "c", "c", "c", 0, 0, 40, 24, 33, 7, 0, ctype))
         out.append((f"zcz_ct{ctype}_fast_op10", "z", "c", "z", 1, 0, 30, 26, 40, 10, 1, ctype))
         out.append((f"zzz_ct{ctype}_fast_N20", "z", "z", "z", 0, 0, 24, 20, 70, 20, 1, ctype))
+    # accurate mode, op C pinned where the reference is deterministic and correct: square shapes
+    # for op(A) = C (big matrix), complex-float output for classic / Karatsuba (their C is written)
+    out.append(("zzz_ct1_accu_op20_sq", "z", "z", "z", 2, 0, 33, 33, 44, 12, 0, 1))
+    out.append(("zzz_ct1_accu_op22_sq", "z", "z", "z", 2, 2, 33, 33, 45, 12, 0, 1))
+    out.append(("ccc_ct1_accu_op22_sq", "c", "c", "c", 2, 2, 40, 40, 36, 7, 0, 1))
+    out.append(("zzz_ct1_accu_op02_k0", "z", "z", "z", 0, 2, 37, 29, 48, 12, 0, 1))
+    for ctype in (2, 3):
+        for opA, opB in ((1, 0), (0, 1), (0, 2), (1, 2)):
+            out.append((f"ccc_ct{ctype}_accu_op{opA}{opB}", "c", "c", "c", opA, opB, 40, 24, 36, 7, 0, ctype))
     return out
 
 

@@ -62,8 +62,7 @@ def test_work_size_and_errors_host_only():
     assert lib.gemmul8_gemm(*args(21)) == -1
     assert lib.gemmul8_gemm(*args(14, ta=2)) == -2          # complex A with real B
     assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2)) == -2  # complex types need COMPLEX_BIG_MATRIX_ENCODE
-    # complex accurate mode is restated for op N x op N only
-    assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2, ct=3, opa=1, fast=0)) == -5
+    assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2, ct=1, opa=3, fast=0)) == -3  # op out of range
     assert lib.gemmul8_gemm(*args(14, k=(1 << 17) + 1)) == -4
 
 

@@ -199,6 +199,18 @@ def test_complex_accurate(ctype, dt, N, k):
     check_full(A, B, N, fast=False, ctype=ctype)
 
 
+@pytest.mark.parametrize("ctype", [1, 2, 3])
+@pytest.mark.parametrize("opA,opB", [(1, 0), (2, 0), (0, 1), (0, 2), (1, 2), (2, 1), (2, 2), (1, 1)])
+def test_complex_accurate_ops(ctype, opA, opB):
+    """complex accurate mode with op T / op C: shifts, slices, residues and C
+    against the oracle; k mod 4 = 2 and 3 cover the tail handling of every extraction"""
+    rng = np.random.default_rng(300 + 30 * ctype + 3 * opA + opB)
+    for dt, m, n, k, N in ((np.complex128, 41, 35, 62, 12), (np.complex64, 30, 30, 47, 7)):
+        A = randmat_np(rng, k, m, dtype=dt) if opA else randmat_np(rng, m, k, dtype=dt)
+        B = randmat_np(rng, n, k, dtype=dt) if opB else randmat_np(rng, k, n, dtype=dt)
+        check_full(A, B, N, fast=False, opA=opA, opB=opB, ctype=ctype)
+
+
 @pytest.mark.parametrize("ctype", [2, 3])
 def test_classic_karatsuba_fast(ctype):
     rng = np.random.default_rng(77 + ctype)

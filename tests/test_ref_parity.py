@@ -44,6 +44,9 @@ CODES = {"d": 0, "s": 1, "z": 2, "c": 3}
     ("z", "z", "z", 600, 500, 700, 12, 1, 2, 1, 1),    # complex op C x op T
     ("z", "z", "z", 250, 300, 301, 12, 0, 0, 0, 1),    # complex accurate, k mod 4 = 1 (m = 256 hits a reference defect)
     ("c", "c", "c", 512, 384, 500, 7, 0, 0, 0, 3),     # Karatsuba, accurate
+    ("z", "z", "z", 250, 300, 301, 12, 0, 0, 2, 1),    # complex accurate, op N x op C
+    ("z", "z", "z", 300, 300, 401, 12, 0, 2, 2, 1),    # complex accurate, op C x op C (square: DESIGN 10.12)
+    ("c", "c", "c", 400, 320, 500, 7, 0, 1, 2, 3),     # Karatsuba accurate, op T x op C
     ("c", "c", "c", 300, 256, 333, 6, 1, 1, 2, 2),     # classic, op T x op C
     ("d", "d", "d", 8192, 8192, 8192, 14, 1, 0, 0, 0),   # cfg2
     ("s", "s", "s", 1024, 1024, 1024, 4, 1, 0, 0, 0),     # cfg1 shape on the GPU
