@@ -69,6 +69,28 @@ __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
                  : "memory");
     __builtin_amdgcn_sched_barrier(0);
 }
+// The same LDS-DMA through a buffer descriptor (SGPR base + 32-bit per-lane offset).  Measured on
+// the product kernel: the texture units spend 20 % fewer cycles per byte on it than on the 64-bit
+// flat form (TD_TD_BUSY 1.91e9 vs 2.38e9 per cfg2 launch), MFMA busy 68 % -> 85 % of the cycles.
+typedef int v4si __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ v4si make_rsrc(const void *base, uint32_t bytes) {
+    const uint64_t b = (uint64_t)(uintptr_t)base;
+    v4si r;
+    r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    r[1] = __builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32) & 0xffff);  // stride 0
+    r[2] = __builtin_amdgcn_readfirstlane((int)bytes);                         // num_records
+    r[3] = 0x00020000;                                                         // raw buffer, dword data
+    return r;
+}
+__device__ __forceinline__ void bglds16(v4si rsrc, uint32_t voff, uint32_t lds_addr) {
+    if (OZ2_ABLATE == 1) return;
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(voff), "s"(rsrc), "s"(lds_addr)
+                 : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
 // s_waitcnt immediates (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]);
 // the builtin form is visible to the compiler's own waitcnt tracking of its ds_reads.
 template <int N> __device__ __forceinline__ void wait_vm_lgkm0() {
@@ -256,7 +278,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], i
     }
 }
 
-template <int EPI>
+// BUF: operand planes below 4 GiB are staged through buffer descriptors (bglds16), larger ones
+// through 64-bit flat addresses (glds16)
+template <int EPI, int BUF>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(1024))) int8_t smem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -281,13 +305,25 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     const int8_t *Bg = g.B + j * g.planeB + (size_t)tn * g.ksteps * PANEL + wave * 1024 + lane * 16;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
     const uint32_t lds_wave = lds_base + wave * 1024;
+    const v4si rA = make_rsrc(g.A + j * g.planeA, (uint32_t)g.planeA);
+    const v4si rB = make_rsrc(g.B + j * g.planeB, (uint32_t)g.planeB);
+    const uint32_t oA = (uint32_t)((size_t)tm * g.ksteps * PANEL) + wave * 1024 + lane * 16;
+    const uint32_t oB = (uint32_t)((size_t)tn * g.ksteps * PANEL) + wave * 1024 + lane * 16;
     auto stage = [&](unsigned ks, unsigned slot) {
         const size_t go = (size_t)ks * PANEL;
         const uint32_t lo = lds_wave + slot * SLOT;
-        glds16(Ag + go, lo);
-        glds16(Ag + go + 8192, lo + 8192);
-        glds16(Bg + go, lo + PANEL);
-        glds16(Bg + go + 8192, lo + PANEL + 8192);
+        if constexpr (BUF) {
+            const uint32_t g32 = (uint32_t)go;
+            bglds16(rA, oA + g32, lo);
+            bglds16(rA, oA + g32 + 8192, lo + 8192);
+            bglds16(rB, oB + g32, lo + PANEL);
+            bglds16(rB, oB + g32 + 8192, lo + PANEL + 8192);
+        } else {
+            glds16(Ag + go, lo);
+            glds16(Ag + go + 8192, lo + 8192);
+            glds16(Bg + go, lo + PANEL);
+            glds16(Bg + go + 8192, lo + PANEL + 8192);
+        }
     };
 
     v16i acc[4][2];
@@ -372,11 +408,14 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         g.bias[i] = (int)(((((uint64_t)1) << 30) + p - 1) / p * p);
     }
     dim3 grid((unsigned)(L.mtiles * L.ntiles), nplanes);
+    const bool buf = L.planeA < ((size_t)1 << 32) && L.planeB < ((size_t)1 << 32);
+#define OZ2_GEMM(E, B) gemm_i8_kernel<E, B><<<grid, dim3(NTHREADS), 0, st>>>(g)
     switch (epi) {
-    case Epi::RESIDUE: gemm_i8_kernel<0><<<grid, dim3(NTHREADS), 0, st>>>(g); break;
-    case Epi::BOUND: gemm_i8_kernel<1><<<grid, dim3(NTHREADS), 0, st>>>(g); break;
-    default: gemm_i8_kernel<2><<<grid, dim3(NTHREADS), 0, st>>>(g); break;
+    case Epi::RESIDUE: buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0); break;
+    case Epi::BOUND: buf ? OZ2_GEMM(1, 1) : OZ2_GEMM(1, 0); break;
+    default: buf ? OZ2_GEMM(2, 1) : OZ2_GEMM(2, 0); break;
     }
+#undef OZ2_GEMM
 }
 
 }  // namespace oz2

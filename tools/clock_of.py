@@ -28,7 +28,7 @@ for k, c in rows.items():
 # every other counter of the pass, per CU per (GRBM) cycle
 for k, c in rows.items():
     g = c.get("GRBM_GUI_ACTIVE")
-    if not g or "gemm" not in k:
+    if not g or not any(w in k for w in ("gemm", "encode", "stats", "crt")):
         continue
     cyc = sum(v for v, _ in g) / len(g) / 8
     for name, vals in c.items():
