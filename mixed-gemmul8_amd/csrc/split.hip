@@ -19,7 +19,39 @@
 
 namespace oz2 {
 
-enum : int { ENC_CONJ = 1, ENC_BTAIL = 2 };
+enum : int { ENC_CONJ = 1, ENC_BTAIL = 2, ENC_KFIRST = 4 };
+#ifndef OZ2_ENC_ABLATE
+#define OZ2_ENC_ABLATE 0  // probe builds only (tools/probes/enc_probe.hip)
+#endif
+
+// f64 residues in groups of up to three moduli.  mod_8i (scaling.hpp:215-223) reduces the
+// integer-valued x with one f64 step per modulus (x - rint(x/p)*p) and finishes in f32.  Both
+// steps are exact, so the result is THE symmetric residue of x (for p = 256 the two ties
+// +-128 are the same byte).  Reducing x once modulo P = p_a p_b p_c (< 2^24: the f64 step is
+// exact and |x mod P| <= P/2 < 2^23 is exact in f32) and then each p from that f32 value with
+// the same two f32 steps yields the same residues with a third of the f64 work.
+struct ModGroups {
+    int ng;
+    int start[OZ2_MAX_MODULI + 1];
+    double P[OZ2_MAX_MODULI];
+    double rP[OZ2_MAX_MODULI];
+};
+static ModGroups make_groups(const ModParams &MP) {
+    ModGroups G{};
+    unsigned j = 0;
+    while (j < MP.N) {
+        const unsigned e = j + 3 < MP.N ? j + 3 : MP.N;
+        double P = 1.0;
+        for (unsigned i = j; i < e; ++i) P *= (double)(MP.p[i] > 0 ? MP.p[i] : 256);
+        G.start[G.ng] = (int)j;
+        G.P[G.ng] = P;
+        G.rP[G.ng] = 1.0 / P;
+        ++G.ng;
+        j = e;
+    }
+    G.start[G.ng] = (int)MP.N;
+    return G;
+}
 
 template <typename R> __device__ __forceinline__ R fma_ru(R a, R b, R c);
 template <> __device__ __forceinline__ double fma_ru<double>(double a, double b, double c) { return __fma_ru(a, b, c); }
@@ -215,11 +247,16 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                                                                    size_t len, const int16_t *__restrict__ sft,
                                                                    int8_t *__restrict__ out, size_t plane,
                                                                    size_t ksteps, size_t kblk, size_t vmax,
-                                                                   int flags, ModParams MP) {
+                                                                   int flags, ModParams MP, ModGroups G) {
     constexpr int KT = CPLX ? 32 : 64;
     constexpr int NT = CPLX ? 128 : 256;
     constexpr int NC = CPLX ? 2 : 1;
-    const size_t v0 = (size_t)blockIdx.x * 64, e0 = (size_t)blockIdx.y * KT;
+    // contiguous vectors: blockIdx.x walks k so that co-running blocks read neighbouring 512-B
+    // pieces of the same vectors (walking the vectors instead puts every co-running block at
+    // the same offset modulo the vector stride, i.e. on the same HBM channels)
+    const bool kfirst = CONTIG && (flags & ENC_KFIRST);
+    const size_t v0 = (size_t)(kfirst ? blockIdx.y : blockIdx.x) * 64;
+    const size_t e0 = (size_t)(kfirst ? blockIdx.x : blockIdx.y) * KT;
     const int tid = threadIdx.x;
     __shared__ R tile[KT][64 + 1][NC];
 
@@ -228,7 +265,13 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
     constexpr int NL = (64 * KT) / NT;
     const bool interior = v0 + 64 <= nvec && e0 + KT <= len;
     R lre[NL], lim[NL];
-    if (interior) {  // block-uniform branch: one batch of unguarded loads
+    if (OZ2_ENC_ABLATE == 2) {  // probe builds only: no loads
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            lre[i] = (R)(tid * 37 + i * 1.25 + v0);
+            lim[i] = 0;
+        }
+    } else if (interior) {  // block-uniform branch: one batch of unguarded loads
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
             const int idx = tid + NT * i;
@@ -337,40 +380,29 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
         return;
     }
 
-    for (unsigned j = 0; j < MP.N; ++j) {
+    // one plane: residues of the 16 elements from their f32 reductions t (tail of mod_8i,
+    // scaling.hpp:218-222, on packed pairs) -> bytes -> emit
+    auto plane_from = [&](unsigned j, const float (&tr)[16], const float (&tim)[16]) {
         const int p = MP.p[j];
-        const double rd = MP.rinv_d[j];
         const float rf = MP.rinv_f[j];
-        // residues of the 16 elements: mod8_f64 (scaling.hpp:215-223) as its f64 head per element
-        // and its two f32 steps on packed pairs; mod8_f32 (:225-230) per element
+        const float pf = -(float)p;
         int rr[16], ri[16];
-        if constexpr (std::is_same<R, double>::value) {
-            float tr[16], tim[16];
 #pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                tr[q] = mod8_head_f64(yr[q], p, rd);
-                tim[q] = CPLX ? mod8_head_f64(yi[q], p, rd) : 0.0f;
+        for (int q = 0; q < 16; q += 2) {
+            const f2v a = mod8_tail_x2(f2v{tr[q], tr[q + 1]}, rf, pf);
+            rr[q] = (int)a.x;
+            rr[q + 1] = (int)a.y;
+            if (CPLX) {
+                const f2v b = mod8_tail_x2(f2v{tim[q], tim[q + 1]}, rf, pf);
+                ri[q] = (int)b.x;
+                ri[q + 1] = (int)b.y;
+            } else {
+                ri[q] = ri[q + 1] = 0;
             }
-            const float pf = -(float)p;
+        }
+        if (OZ2_ENC_ABLATE == 1) {  // probe builds only: no residue arithmetic
 #pragma unroll
-            for (int q = 0; q < 16; q += 2) {
-                const f2v a = mod8_tail_x2(f2v{tr[q], tr[q + 1]}, rf, pf);
-                rr[q] = (int)a.x;
-                rr[q + 1] = (int)a.y;
-                if (CPLX) {
-                    const f2v b = mod8_tail_x2(f2v{tim[q], tim[q + 1]}, rf, pf);
-                    ri[q] = (int)b.x;
-                    ri[q + 1] = (int)b.y;
-                } else {
-                    ri[q] = ri[q + 1] = 0;
-                }
-            }
-        } else {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                rr[q] = mod8_f32(yr[q], p, rf);
-                ri[q] = CPLX ? mod8_f32(yi[q], p, rf) : 0;
-            }
+            for (int q = 0; q < 16; ++q) rr[q] = (int)tr[q] + p;
         }
         uint32_t wr[4], wi[4];
 #pragma unroll
@@ -385,6 +417,44 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
             wi[d] = ai;
         }
         emit(out + (size_t)j * plane, wr, wi);
+    };
+
+    if constexpr (std::is_same<R, double>::value) {
+        for (int gi = 0; gi < G.ng; ++gi) {
+            const double P = G.P[gi], rP = G.rP[gi];
+            float tr[16], tim[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                tr[q] = __double2float_rn(__builtin_fma(__builtin_rint(yr[q] * rP), -P, yr[q]));
+                tim[q] = CPLX ? __double2float_rn(__builtin_fma(__builtin_rint(yi[q] * rP), -P, yi[q])) : 0.0f;
+            }
+            for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from((unsigned)j, tr, tim);
+        }
+    } else {
+        // f32 operands: mod_8i's four f32 steps per modulus (scaling.hpp:225-230)
+        for (unsigned j = 0; j < MP.N; ++j) {
+            const int p = MP.p[j];
+            const float rf = MP.rinv_f[j];
+            int rr[16], ri[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                rr[q] = mod8_f32(yr[q], p, rf);
+                ri[q] = CPLX ? mod8_f32(yi[q], p, rf) : 0;
+            }
+            uint32_t wr[4], wi[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                uint32_t ar = 0, ai = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    ar |= ((uint32_t)rr[4 * d + b] & 0xffu) << (8 * b);
+                    ai |= ((uint32_t)ri[4 * d + b] & 0xffu) << (8 * b);
+                }
+                wr[d] = ar;
+                wi[d] = ai;
+            }
+            emit(out + (size_t)j * plane, wr, wi);
+        }
     }
 }
 
@@ -426,8 +496,12 @@ static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, si
     constexpr int KT = CPLX ? 32 : 64;
     constexpr int NT = CPLX ? 128 : 256;
     const R *x = static_cast<const R *>(X);
-    dim3 grid((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
-#define OZ2_EN(cg, md) encode_kernel<R, CPLX, cg, IS_A, md><<<grid, dim3(NT), 0, st>>>(x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP)
+    const bool kf = contig;  // k-first block order for contiguous vectors (-4.5 % on B, see encode_kernel)
+    if (kf) flags |= ENC_KFIRST;
+    const dim3 grid = kf ? dim3((unsigned)(L.kblk / KT), (unsigned)(vpad_grid / 64))
+                         : dim3((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
+    const ModGroups G = make_groups(MP);
+#define OZ2_EN(cg, md) encode_kernel<R, CPLX, cg, IS_A, md><<<grid, dim3(NT), 0, st>>>(x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G)
     if (contig) { if (mode == 0) OZ2_EN(true, 0); else OZ2_EN(true, 1); }
     else { if (mode == 0) OZ2_EN(false, 0); else OZ2_EN(false, 1); }
 #undef OZ2_EN
