@@ -58,7 +58,8 @@ struct GemmArgs {
 // so the compiler neither waits for it nor reorders it; completion is counted with vmcnt by hand.
 // M0 is compiler-reserved: saved and restored inside the statement.
 #ifndef OZ2_ABLATE
-#define OZ2_ABLATE 0  // probe builds only: 1 = no LDS-DMA in the main loop, 2 = no MFMA, 3 = no LDS reads
+#define OZ2_ABLATE 0  // probe builds only: 1 = no LDS-DMA, 2 = no MFMA, 3 = no LDS reads, 5 = LDS reads of the first
+                     // step only, 6 = LDS-DMA of the prologue only (real operands, no data movement in the loop)
 #endif
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
     if (OZ2_ABLATE == 1) return;
@@ -166,15 +167,15 @@ __device__ __forceinline__ void mfma_step(v16i (&acc)[4][2], const Frags &f) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int jj = 0; jj < 2; ++jj) {
-                if (OZ2_ABLATE == 2 || OZ2_ABLATE == 4) {
-                    acc[i][jj][0] += f.a[s][i][0] ^ f.b[s][jj][1];
-                } else {
-                    acc[i][jj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.a[s][i], f.b[s][jj], acc[i][jj], 0, 0, 0);
-                }
+        for (int x = 0; x < 8; ++x) {
+            const int i = x >> 1, jj = x & 1;  // (serpentine orders that share an operand between
+                                               // consecutive MFMAs measured the same clock)
+            if (OZ2_ABLATE == 2 || OZ2_ABLATE == 4) {
+                acc[i][jj][0] += f.a[s][i][0] ^ f.b[s][jj][1];
+            } else {
+                acc[i][jj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.a[s][i], f.b[s][jj], acc[i][jj], 0, 0, 0);
             }
+        }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
 }
@@ -355,10 +356,15 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
         Frags f;
         unsigned slot_cur = 0, slot_issue = D % STAGES;
         unsigned t = 0;
+        if (OZ2_ABLATE == 6 && K > D) {  // probe: every ring slot filled once, no DMA in the loop
+            stage(D, D % STAGES);
+            wait_vm_lgkm0<0>();
+            barrier();
+        }
         for (; t + D < K; ++t) {  // steady state
-            read_frags(f, smem + slot_cur * SLOT, wr, wc, lane);
+            if (OZ2_ABLATE != 5 || t == 0) read_frags(f, smem + slot_cur * SLOT, wr, wc, lane);  // 5: reads once
             __builtin_amdgcn_sched_barrier(0);
-            stage(t + D, slot_issue);
+            if (OZ2_ABLATE != 6) stage(t + D, slot_issue);
             wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();
             barrier();
             mfma_step(acc, f);
