@@ -414,7 +414,9 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         g.bias[i] = (int)(((((uint64_t)1) << 30) + p - 1) / p * p);
     }
     dim3 grid((unsigned)(L.mtiles * L.ntiles), nplanes);
-    const bool buf = L.planeA < ((size_t)1 << 32) && L.planeB < ((size_t)1 << 32);
+    // GEMMUL8_FORCE_FLAT_DMA=1 takes the 64-bit path at any size (tests cover it with small shapes)
+    const char *ff = getenv("GEMMUL8_FORCE_FLAT_DMA");
+    const bool buf = L.planeA < ((size_t)1 << 32) && L.planeB < ((size_t)1 << 32) && !(ff && atoi(ff));
 #define OZ2_GEMM(E, B) gemm_i8_kernel<E, B><<<grid, dim3(NTHREADS), 0, st>>>(g)
     switch (epi) {
     case Epi::RESIDUE: buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0); break;

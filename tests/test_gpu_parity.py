@@ -253,3 +253,14 @@ def test_mfma_raw_product():
     got = C32.cpu().numpy().T  # (m_pad, n_pad)
     exp = A8.astype(np.int64) @ B8.astype(np.int64).T
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_flat_address_dma_path(fast, monkeypatch):
+    """the product kernel's 64-bit flat LDS-DMA path (taken for slice planes of 4 GiB and more)
+    forced at small sizes: same slices, residues and C as the oracle"""
+    monkeypatch.setenv("GEMMUL8_FORCE_FLAT_DMA", "1")
+    rng = np.random.default_rng(61 + fast)
+    check_full(randmat_np(rng, 300, 513), randmat_np(rng, 513, 260), 14, fast=fast)
+    check_full(randmat_np(rng, 45, 70, dtype=np.complex128), randmat_np(rng, 70, 38, dtype=np.complex128), 12,
+               fast=fast)
