@@ -95,9 +95,18 @@ def cpu_baseline(size_hint):
     t0 = time.perf_counter()
     O.gemm(A, A, 14, True)
     dt = time.perf_counter() - t0
+    model = "unknown CPU"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
     return {"value": 2.0 * n ** 3 / dt / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
             "sample": f"DGEMM emulation m=n=k={n}, num_moduli=14, fast mode, one call ({dt:.1f} s) of the "
-                      f"oracle/oz2_oracle.c restatement with {threads} OpenMP threads"}
+                      f"oracle/oz2_oracle.c restatement with {threads} OpenMP threads on {model} "
+                      f"({os.cpu_count()} logical CPUs visible)"}
 
 
 def traffic_from_profile():
