@@ -495,6 +495,7 @@ static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, si
                           int flags, const ModParams &MP, hipStream_t st) {
     constexpr int KT = CPLX ? 32 : 64;
     constexpr int NT = CPLX ? 128 : 256;
+    if (L.kblk == 0 || vpad_grid == 0) return;  // k = 0: the slice planes are empty
     const R *x = static_cast<const R *>(X);
     const bool kf = contig;  // k-first block order for contiguous vectors (-4.5 % on B, see encode_kernel)
     if (kf) flags |= ENC_KFIRST;

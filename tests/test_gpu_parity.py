@@ -264,3 +264,24 @@ def test_flat_address_dma_path(fast, monkeypatch):
     check_full(randmat_np(rng, 300, 513), randmat_np(rng, 513, 260), 14, fast=fast)
     check_full(randmat_np(rng, 45, 70, dtype=np.complex128), randmat_np(rng, 70, 38, dtype=np.complex128), 12,
                fast=fast)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_empty_k(fast):
+    """k = 0: every residue is 0, so C = beta * C (alpha * 0 + beta * C)"""
+    rng = np.random.default_rng(71)
+    A = np.zeros((40, 0), np.float64, order="F")
+    B = np.zeros((0, 30), np.float64, order="F")
+    C0 = randmat_np(rng, 40, 30)
+    C, _, _ = run_gpu(A, B, 14, fast=fast, alpha=2.0, beta=-0.5, C0=C0)
+    assert np.array_equal(C, -0.5 * C0)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_long_k_signed_residue_path(fast):
+    """k_pad > 2^16: the int32 products may exceed 2^30, so the epilogue takes the reference's
+    signed Barrett reduction (conv_32i_2_8u.hpp:7-71) instead of the biased one"""
+    rng = np.random.default_rng(72 + fast)
+    check_full(randmat_np(rng, 20, 70000), randmat_np(rng, 70000, 24), 14, fast=fast)
+    check_full(randmat_np(rng, 12, 40000, dtype=np.complex128), randmat_np(rng, 40000, 10, dtype=np.complex128), 12,
+               fast=fast)
