@@ -32,6 +32,11 @@ for name, dt, (m, k, n) in (("d", torch.float64, (512, 448, 384)), ("z", torch.c
     exact = (A.cpu().to(torch.complex128) @ B.cpu().to(torch.complex128))
     out[name] = {"bits": bool(torch.equal(C, E)),
                  "relerr": float(((C.cpu().to(torch.complex128) - exact).abs() / exact.abs()).max())}
+Ab = torch.randn(3, 300, 260, dtype=torch.float64, device="cuda", generator=g)
+Bb = torch.randn(3, 260, 280, dtype=torch.float64, device="cuda", generator=g)
+Cb = torch.bmm(Ab, Bb)                           # -> hipblasDgemmStridedBatched -> interposer
+Eb = torch.stack([G.matmul(Bb[i].t().contiguous(), Ab[i].t().contiguous(), 14).t() for i in range(3)])
+out["bmm_bits"] = bool(torch.equal(Cb, Eb))
 A = torch.randn(64, 64, dtype=torch.float64, device="cuda", generator=g)
 C = A @ A                                        # below the thresholds: forwarded
 out["small_relerr"] = float(((C - (A.cpu() @ A.cpu()).cuda()).abs().max() / (A.cpu() @ A.cpu()).abs().max()))
@@ -52,5 +57,7 @@ def test_torch_matmul_is_emulated():
     assert "[gemmul8] hipblasZgemm m=280 n=300 k=260 -> emulated" in log, log[-2000:]
     assert "m=64 n=64" not in log  # below the intercept thresholds: never reaches the emulator
     assert res["d"]["bits"] and res["z"]["bits"], res
+    assert "[gemmul8] hipblasDgemmStridedBatched m=280 n=300 k=260" in log, log[-2000:]
+    assert res["bmm_bits"], res
     assert res["d"]["relerr"] < 1e-9 and res["z"]["relerr"] < 1e-9, res
     assert res["small_relerr"] < 1e-12, res

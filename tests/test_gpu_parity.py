@@ -285,3 +285,26 @@ def test_long_k_signed_residue_path(fast):
     check_full(randmat_np(rng, 20, 70000), randmat_np(rng, 70000, 24), 14, fast=fast)
     check_full(randmat_np(rng, 12, 40000, dtype=np.complex128), randmat_np(rng, 40000, 10, dtype=np.complex128), 12,
                fast=fast)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_padded_leading_dimensions(fast):
+    """lda > m, ldb > k, ldc > m (odd, so C columns are not 16-byte aligned): same bits as the
+    tight layout, and C's padding rows are left untouched"""
+    torch = _torch()
+    import gemmul8 as G
+    rng = np.random.default_rng(81 + fast)
+    m, n, k, N = 130, 70, 150, 14
+    A, B = randmat_np(rng, m, k), randmat_np(rng, k, n)
+    C_tight, _, _ = run_gpu(A, B, N, fast=fast)
+    lda, ldb, ldc = m + 7, k + 3, m + 5
+    Ap = np.zeros((lda, k), order="F"); Ap[:m] = A
+    Bp = np.zeros((ldb, n), order="F"); Bp[:k] = B
+    Cp = np.full((ldc, n), 7.0, order="F")
+    dA, dB, dC = to_dev(Ap), to_dev(Bp), to_dev(Cp)
+    work = G.alloc_work(m, n, k, N)
+    G.gemm(0, 0, m, n, k, 1.0, dA, lda, dB, ldb, 0.0, dC, ldc, N, fast, work)
+    torch.cuda.synchronize()
+    Cg = np.asfortranarray(dC.cpu().numpy().T)
+    assert Cg[:m].tobytes() == C_tight.tobytes()
+    assert np.all(Cg[m:] == 7.0)
