@@ -60,8 +60,15 @@ def dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
+        # one GPU per rank; GEMMUL8_BENCH_BACKEND=gloo (with ranks sharing a device) rehearses the
+        # multi-rank flow on a one-GPU box -- timing from such a run means nothing
+        backend = os.environ.get("GEMMUL8_BENCH_BACKEND", "nccl")
+        local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank
@@ -78,7 +85,8 @@ def max_over_ranks(x, world):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
