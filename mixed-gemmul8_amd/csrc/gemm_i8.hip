@@ -389,6 +389,59 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
 }
 
 
+// Exhaustive check of the two residue epilogues against exact arithmetic, every input and every
+// modulus: path 0 = biased (x in [-2^30, 2^30], the accumulator starting at bias_i), path 1 = signed
+// Barrett (every int32, conv_32i_2_8u.hpp:7-56).  Counts mismatches into *count.
+__global__ void residue_selftest_kernel(int path, GemmArgs g, unsigned long long *count) {
+    unsigned long long bad = 0;
+    // path 2: the biased check against a deliberately wrong expectation (negative control: every
+    // pair must be counted)
+    const uint64_t total = path != 1 ? ((uint64_t)1 << 31) + 1 : ((uint64_t)1 << 32);
+    const int64_t lo = path != 1 ? -((int64_t)1 << 30) : -((int64_t)1 << 31);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+        const int64_t x = lo + (int64_t)i;
+        for (int j = 0; j < OZ2_MAX_MODULI; ++j) {
+            const int p = g.p[j] > 0 ? g.p[j] : 256;
+            // exact x mod p in [0, p) through f64 (|x| < 2^53) with a one-step correction
+            int64_t q = (int64_t)floor((double)x * (1.0 / (double)p));
+            int64_t r = x - q * p;
+            if (r < 0) r += p;
+            if (r >= p) r -= p;
+            if (path == 2) r = (r + 1) % p;
+            uint32_t got;
+            if (path != 1) got = residue_biased((uint32_t)((int32_t)x + g.bias[j]), (uint32_t)p, g.minv[j]);
+            else got = residue((int)x, g.p[j], g.barrett[j], p == 256);
+            bad += (got != (uint32_t)r);
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) bad += __shfl_xor(bad, d);
+    if ((threadIdx.x & 63) == 0 && bad) atomicAdd(count, bad);
+}
+
+unsigned long long residue_selftest(int path, hipStream_t st) {
+    GemmArgs g{};
+    const ModParams MP = make_mod_params(OZ2_MAX_MODULI);
+    for (int i = 0; i < OZ2_MAX_MODULI; ++i) {
+        g.p[i] = MP.p[i];
+        g.barrett[i] = MP.barrett[i];
+        const uint32_t p = MP.p[i] > 0 ? (uint32_t)MP.p[i] : 256u;
+        g.minv[i] = (uint32_t)((((uint64_t)1) << 32) / p);
+        g.bias[i] = (int)(((((uint64_t)1) << 30) + p - 1) / p * p);
+    }
+    unsigned long long *d = nullptr, h = ~0ull;
+    if (hipMalloc(&d, sizeof(h)) != hipSuccess) return h;
+    (void)hipMemsetAsync(d, 0, sizeof(h), st);
+    residue_selftest_kernel<<<4096, 256, 0, st>>>(path, g, d);
+    if (hipGetLastError() != hipSuccess) {
+        (void)hipFree(d);
+        return ~0ull;
+    }
+    (void)hipMemcpyAsync(&h, d, sizeof(h), hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(d);
+    return h;
+}
+
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
              int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st) {
     GemmArgs g{};

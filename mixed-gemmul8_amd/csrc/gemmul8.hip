@@ -423,6 +423,10 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
     return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
 
+unsigned long long gemmul8_residue_selftest(void *stream, int path) {
+    return oz2::residue_selftest(path, static_cast<hipStream_t>(stream));
+}
+
 }  // extern "C"
 
 // =========================== drop-in C++ API ===============================

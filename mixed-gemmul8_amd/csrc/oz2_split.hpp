@@ -36,6 +36,8 @@ enum class Epi : int { RESIDUE = 0, BOUND = 1, RAW = 2 };
 // bound (rowmax[m_pad], colmax[n_pad] of |C|, must be zeroed), or raw int32 (plane 0 only).
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
              int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st);
+// exhaustive exactness check of the residue epilogues (0 = biased, 1 = signed): mismatch count
+unsigned long long residue_selftest(int path, hipStream_t st);
 
 // ---- crt.hip ----
 enum class OutType : int { F64 = 0, F32 = 1, C64 = 2, C32 = 3 };

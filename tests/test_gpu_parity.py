@@ -308,3 +308,17 @@ def test_padded_leading_dimensions(fast):
     Cg = np.asfortranarray(dC.cpu().numpy().T)
     assert Cg[:m].tobytes() == C_tight.tobytes()
     assert np.all(Cg[m:] == 7.0)
+
+
+@pytest.mark.parametrize("path", [0, 1])
+def test_residue_epilogue_exhaustive(path):
+    """every input of both residue reductions of the product epilogue, all 20 moduli, against exact
+    arithmetic: the biased form over x in [-2^30, 2^30] (k_pad <= 2^16) and the reference's signed
+    Barrett step (conv_32i_2_8u.hpp:7-56) over every int32 -- 8.6e10 and 1.7e11 checks"""
+    import ctypes
+    import gemmul8 as G
+    G.lib.gemmul8_residue_selftest.restype = ctypes.c_ulonglong
+    G.lib.gemmul8_residue_selftest.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    assert G.lib.gemmul8_residue_selftest(G._stream(), path) == 0
+    if path == 0:  # negative control: a wrong expectation is counted for every (input, modulus) pair
+        assert G.lib.gemmul8_residue_selftest(G._stream(), 2) == ((1 << 31) + 1) * 20
