@@ -59,7 +59,8 @@ struct GemmArgs {
 // M0 is compiler-reserved: saved and restored inside the statement.
 #ifndef OZ2_ABLATE
 #define OZ2_ABLATE 0  // probe builds only: 1 = no LDS-DMA, 2 = no MFMA, 3 = no LDS reads, 5 = LDS reads of the first
-                     // step only, 6 = LDS-DMA of the prologue only (real operands, no data movement in the loop)
+                     // step only, 6 = LDS-DMA of the prologue only (real operands, no data movement in the loop),
+                     // 7 = residue epilogue reduced to the low byte
 #endif
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
     if (OZ2_ABLATE == 1) return;
@@ -208,7 +209,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], i
                     __builtin_amdgcn_sched_barrier(0);
                 }
         };
-        if (g.biased) {
+        if (OZ2_ABLATE == 7) {  // probe: the low byte only (cost of the mod-p reduction)
+            park([&](int x) { return (uint32_t)x & 0xffu; });
+        } else if (g.biased) {
             const uint32_t m = g.minv[j];
             park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
         } else {

@@ -16,6 +16,7 @@
 // Accurate mode adds the 6-bit magnitude extraction (scaling.hpp:1897-1941,
 // 2215-2260) whose bound product runs on the int8 GEMM kernel (gemm_i8.hip).
 #include "oz2_split.hpp"
+#include <cstdlib>
 
 namespace oz2 {
 
@@ -162,33 +163,52 @@ __global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ 
 }
 
 // ------------------------------------------------------------------
-// pass 1b: strided vectors (A op N, B op T): 16 vectors per 256-thread block,
-// coalesced 16-row sweeps; virtual thread t of the reference = slot + 16*c
+// pass 1b: strided vectors (A op N, B op T): ROWS vectors per 256-thread block, swept
+// ROWS rows at a time so every wave load is a contiguous run of rows; thread (row, slot)
+// carries the reference's virtual threads t = slot + SLOTS*c (c < NA).  The loads of U
+// consecutive VT-chunks are issued before any of them is accumulated; each chain still
+// consumes its elements in increasing order, so the round-up sums are unchanged.
+// ROWS = 16 for m >= 4096; 8 / 4 below, where m/16 blocks leave CUs idle (1024: 15.2 -> 9.6 us,
+// 2048: 23.2 -> 17.3 us; narrower rows cost HBM efficiency at 4096 and up, tools/probes/run_stats_rows.sh).
 // ------------------------------------------------------------------
-template <typename R, bool CPLX, int VT, bool ACCU>
+template <typename R, bool CPLX, int VT, bool ACCU, int ROWS>
 __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
                                                            float log2M, int16_t *__restrict__ sft_out) {
-    constexpr int NA = VT / 16;
-    const int tid = threadIdx.x, row = tid & 15, slot = tid >> 4;
-    const size_t v = (size_t)blockIdx.x * 16 + row;
+    constexpr int SLOTS = 256 / ROWS;
+    constexpr int NA = VT / SLOTS;
+    constexpr int U = (ROWS == 16 || NA >= 16) ? 1 : 16 / NA;  // batching measured slower at 16 rows
+    static_assert(SLOTS <= 64 && NA >= 1, "one reduction lane per slot");
+    const int tid = threadIdx.x, row = tid % ROWS, slot = tid / ROWS;
+    const size_t v = (size_t)blockIdx.x * ROWS + row;
     R acc[NA];
 #pragma unroll
     for (int c = 0; c < NA; ++c) acc[c] = 0;
     R amax = 0;
     if (v < nvec) {
         size_t b = 0;
-        // full chunks: all NA loads issued before the round-up chains consume them
+        // full groups of U chunks: U*NA loads in flight, then the chains in element order
+        for (; b + (size_t)U * VT <= len; b += (size_t)U * VT) {
+            R re[U][NA], im[U][NA];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int c = 0; c < NA; ++c) load_elem<R, CPLX>(X, (b + u * VT + slot + SLOTS * c) * ld + v, re[u][c], im[u][c]);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int c = 0; c < NA; ++c) accum<R, CPLX>(re[u][c], im[u][c], amax, acc[c]);
+        }
         for (; b + VT <= len; b += VT) {
             R re[NA], im[NA];
 #pragma unroll
-            for (int c = 0; c < NA; ++c) load_elem<R, CPLX>(X, (b + slot + 16 * c) * ld + v, re[c], im[c]);
+            for (int c = 0; c < NA; ++c) load_elem<R, CPLX>(X, (b + slot + SLOTS * c) * ld + v, re[c], im[c]);
 #pragma unroll
             for (int c = 0; c < NA; ++c) accum<R, CPLX>(re[c], im[c], amax, acc[c]);
         }
         for (; b < len; b += VT) {
 #pragma unroll
             for (int c = 0; c < NA; ++c) {
-                const size_t e = b + slot + 16 * c;
+                const size_t e = b + slot + SLOTS * c;
                 if (e < len) {
                     R re, im;
                     load_elem<R, CPLX>(X, e * ld + v, re, im);
@@ -197,20 +217,19 @@ __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict_
             }
         }
     }
-    __shared__ R part[16][VT + 1];
-    __shared__ R pmax[16][17];
+    __shared__ R part[ROWS][VT + 1];
+    __shared__ R pmax[ROWS][SLOTS + 1];
     if (!ACCU) {
 #pragma unroll
-        for (int c = 0; c < NA; ++c) part[row][slot + 16 * c] = acc[c];
+        for (int c = 0; c < NA; ++c) part[row][slot + SLOTS * c] = acc[c];
     }
     pmax[row][slot] = amax;
     __syncthreads();
     const int w = tid >> 6, lane = tid & 63;
 #pragma unroll 1
-    for (int rr = 0; rr < 4; ++rr) {
-        const int r2 = w * 4 + rr;
-        const size_t v2 = (size_t)blockIdx.x * 16 + r2;
-        R mx = lane < 16 ? pmax[r2][lane] : R(0);
+    for (int r2 = w; r2 < ROWS; r2 += 4) {
+        const size_t v2 = (size_t)blockIdx.x * ROWS + r2;
+        R mx = lane < SLOTS ? pmax[r2][lane] : R(0);
         mx = wave_max<R>(mx);
         if (ACCU) {
             if (lane == 0 && v2 < nvec)
@@ -481,10 +500,20 @@ static void launch_stats(const void *X, size_t ld, bool contig, size_t len, size
         else { if (accurate) OZ2_SC(128, true); else OZ2_SC(128, false); }
 #undef OZ2_SC
     } else {
-        const unsigned g = (unsigned)((nvec + 15) / 16);
-#define OZ2_SS(vt, ac) stats_strided_kernel<R, CPLX, vt, ac><<<dim3(g), dim3(256), 0, st>>>(x, ld, len, nvec, log2M, out)
-        if (VT == 512) { if (accurate) OZ2_SS(512, true); else OZ2_SS(512, false); }
-        else { if (accurate) OZ2_SS(128, true); else OZ2_SS(128, false); }
+        // rows per block: enough blocks to give every CU several (m/16 < 2 per CU leaves the
+        // chip latency-bound); GEMMUL8_STATS_ROWS overrides (probe / A-B runs)
+        static const int forced = [] {
+            const char *e = getenv("GEMMUL8_STATS_ROWS");
+            const int r = e ? atoi(e) : 0;
+            return (r == 4 || r == 8 || r == 16) ? r : 0;
+        }();
+        const int rows = forced ? forced : nvec >= 4096 ? 16 : nvec >= 2048 ? 8 : 4;
+        const unsigned g = (unsigned)((nvec + rows - 1) / rows);
+#define OZ2_SS(vt, ac, rw) stats_strided_kernel<R, CPLX, vt, ac, rw><<<dim3(g), dim3(256), 0, st>>>(x, ld, len, nvec, log2M, out)
+#define OZ2_SSR(vt, ac) do { if (rows == 16) OZ2_SS(vt, ac, 16); else if (rows == 8) OZ2_SS(vt, ac, 8); else OZ2_SS(vt, ac, 4); } while (0)
+        if (VT == 512) { if (accurate) OZ2_SSR(512, true); else OZ2_SSR(512, false); }
+        else { if (accurate) OZ2_SSR(128, true); else OZ2_SSR(128, false); }
+#undef OZ2_SSR
 #undef OZ2_SS
     }
 }
