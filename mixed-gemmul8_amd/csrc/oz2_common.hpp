@@ -168,6 +168,15 @@ __device__ __forceinline__ f2v mod8_tail_x2(f2v t, float rinvf, float pf) {
     }
     return t;
 }
+// One such step: the residue of t modulo p when |t/p| < 2^10 (t reduced modulo a two-moduli
+// product first, split.hip ModGroups)
+__device__ __forceinline__ f2v mod8_step_x2(f2v t, float rinvf, float pf) {
+    const f2v c = {12582912.0f, 12582912.0f};
+    const f2v r = {rinvf, rinvf}, q = {pf, pf};
+    f2v y = t * r;
+    y = (y + c) - c;
+    return __builtin_elementwise_fma(y, q, t);
+}
 __device__ __forceinline__ float mod8_head_f64(double x, int p, double rinv) {
     return __double2float_rn(__builtin_fma(__builtin_rint(x * rinv), -(double)p, x));
 }

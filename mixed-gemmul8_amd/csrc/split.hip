@@ -25,23 +25,36 @@ enum : int { ENC_CONJ = 1, ENC_BTAIL = 2, ENC_KFIRST = 4 };
 #define OZ2_ENC_ABLATE 0  // probe builds only (tools/probes/enc_probe.hip)
 #endif
 
-// f64 residues in groups of up to three moduli.  mod_8i (scaling.hpp:215-223) reduces the
-// integer-valued x with one f64 step per modulus (x - rint(x/p)*p) and finishes in f32.  Both
-// steps are exact, so the result is THE symmetric residue of x (for p = 256 the two ties
-// +-128 are the same byte).  Reducing x once modulo P = p_a p_b p_c (< 2^24: the f64 step is
-// exact and |x mod P| <= P/2 < 2^23 is exact in f32) and then each p from that f32 value with
-// the same two f32 steps yields the same residues with a third of the f64 work.
+// f64 residues in groups of moduli.  mod_8i (scaling.hpp:215-223) reduces the integer-valued x
+// with one f64 step per modulus (x - rint(x/p)*p) and finishes in f32.  Both steps are exact, so
+// the result is THE symmetric residue of x (for p = 256 the two ties +-128 are the same byte).
+// Here x is reduced once modulo the product P of a group in f64, and each p of the group then
+// finishes in f32 from that value:
+//   pairs (N <= 17): P < 2^16, |x| < 2^72 (fast: log2M_fast[N] <= 66; accurate: 6 + log2M_accu <= 72),
+//     so rint(x/P) errs by < 2^20 and |t| < 2^22: ONE f32 step is exact (rint(t*fl(1/p)) is off
+//     from t/p by < 2^-23 |t/p|, less than the 1/(2p) separating t/p from a half-integer when p is
+//     odd; p = 256: exact product, a tie gives +-128, one byte);
+//   triples (N >= 18): P < 2^24, two f32 steps (the reference's own two).
+// Same residues as mod_8i either way (tools/probes/modcheck.py checks both forms against exact
+// integers over the magnitude range); per element, 7 f64 steps and 14 packed f32 steps at N = 14.
 struct ModGroups {
     int ng;
+    int steps;  // f32 steps per modulus (1: pairs, 2: triples)
     int start[OZ2_MAX_MODULI + 1];
     double P[OZ2_MAX_MODULI];
     double rP[OZ2_MAX_MODULI];
 };
-static ModGroups make_groups(const ModParams &MP) {
+static ModGroups make_groups(const ModParams &MP, unsigned Ncall) {
     ModGroups G{};
+    static const bool triples = [] {  // GEMMUL8_ENC_TRIPLES=1: the triple form at every N (A-B runs)
+        const char *e = getenv("GEMMUL8_ENC_TRIPLES");
+        return e && atoi(e) != 0;
+    }();
+    const unsigned gs = (Ncall <= 17 && !triples) ? 2 : 3;
+    G.steps = gs == 2 ? 1 : 2;
     unsigned j = 0;
     while (j < MP.N) {
-        const unsigned e = j + 3 < MP.N ? j + 3 : MP.N;
+        const unsigned e = j + gs < MP.N ? j + gs : MP.N;
         double P = 1.0;
         for (unsigned i = j; i < e; ++i) P *= (double)(MP.p[i] > 0 ? MP.p[i] : 256);
         G.start[G.ng] = (int)j;
@@ -399,20 +412,20 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
         return;
     }
 
-    // one plane: residues of the 16 elements from their f32 reductions t (tail of mod_8i,
-    // scaling.hpp:218-222, on packed pairs) -> bytes -> emit
-    auto plane_from = [&](unsigned j, const float (&tr)[16], const float (&tim)[16]) {
+    // one plane: residues of the 16 elements from their f32 reductions t modulo P (one step of
+    // the tail of mod_8i, scaling.hpp:218-222, on packed pairs) -> bytes -> emit
+    auto plane_from = [&]<int STEPS>(unsigned j, const float (&tr)[16], const float (&tim)[16]) {
         const int p = MP.p[j];
         const float rf = MP.rinv_f[j];
         const float pf = -(float)p;
         int rr[16], ri[16];
 #pragma unroll
         for (int q = 0; q < 16; q += 2) {
-            const f2v a = mod8_tail_x2(f2v{tr[q], tr[q + 1]}, rf, pf);
+            const f2v a = STEPS == 1 ? mod8_step_x2(f2v{tr[q], tr[q + 1]}, rf, pf) : mod8_tail_x2(f2v{tr[q], tr[q + 1]}, rf, pf);
             rr[q] = (int)a.x;
             rr[q + 1] = (int)a.y;
             if (CPLX) {
-                const f2v b = mod8_tail_x2(f2v{tim[q], tim[q + 1]}, rf, pf);
+                const f2v b = STEPS == 1 ? mod8_step_x2(f2v{tim[q], tim[q + 1]}, rf, pf) : mod8_tail_x2(f2v{tim[q], tim[q + 1]}, rf, pf);
                 ri[q] = (int)b.x;
                 ri[q + 1] = (int)b.y;
             } else {
@@ -447,7 +460,11 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                 tr[q] = __double2float_rn(__builtin_fma(__builtin_rint(yr[q] * rP), -P, yr[q]));
                 tim[q] = CPLX ? __double2float_rn(__builtin_fma(__builtin_rint(yi[q] * rP), -P, yi[q])) : 0.0f;
             }
-            for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from((unsigned)j, tr, tim);
+            if (G.steps == 1) {
+                for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from.template operator()<1>((unsigned)j, tr, tim);
+            } else {
+                for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from.template operator()<2>((unsigned)j, tr, tim);
+            }
         }
     } else {
         // f32 operands: mod_8i's four f32 steps per modulus (scaling.hpp:225-230)
@@ -530,7 +547,7 @@ static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, si
     if (kf) flags |= ENC_KFIRST;
     const dim3 grid = kf ? dim3((unsigned)(L.kblk / KT), (unsigned)(vpad_grid / 64))
                          : dim3((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
-    const ModGroups G = make_groups(MP);
+    const ModGroups G = make_groups(MP, L.N);  // grouping by the call's N (magnitude bound), not the sub-range
 #define OZ2_EN(cg, md) encode_kernel<R, CPLX, cg, IS_A, md><<<grid, dim3(NT), 0, st>>>(x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G)
     if (contig) { if (mode == 0) OZ2_EN(true, 0); else OZ2_EN(true, 1); }
     else { if (mode == 0) OZ2_EN(false, 0); else OZ2_EN(false, 1); }
