@@ -37,9 +37,15 @@ enum : int { ENC_CONJ = 1, ENC_BTAIL = 2, ENC_KFIRST = 4 };
 //   triples (N >= 18): P < 2^24, two f32 steps (the reference's own two).
 // Same residues as mod_8i either way (tools/probes/modcheck.py checks both forms against exact
 // integers over the magnitude range); per element, 7 f64 steps and 14 packed f32 steps at N = 14.
+// f32 operands: mod_8i<float> (scaling.hpp:225-230) takes four f32 steps from x itself.  For
+// |x| < 2^46 the first step's quotient errs by < 2^23/p, so its fma result is an exact integer
+// below 2^24 and the remaining steps end at THE symmetric residue; |x| < 2^(6 + log2M_accu[N]) <=
+// 2^45.2 holds for N <= 10 in both modes, and there the f64 group form (x converted exactly)
+// gives the same bytes.  Above N = 10 the four f32 steps are kept as they are, rounding included.
 struct ModGroups {
     int ng;
-    int steps;  // f32 steps per modulus (1: pairs, 2: triples)
+    int steps;      // f32 steps per modulus (1: pairs, 2: triples)
+    int f32_exact;  // f32 operands: mod_8i<float>'s four f32 steps are exact (N <= 10), so the f64 form applies
     int start[OZ2_MAX_MODULI + 1];
     double P[OZ2_MAX_MODULI];
     double rP[OZ2_MAX_MODULI];
@@ -52,6 +58,7 @@ static ModGroups make_groups(const ModParams &MP, unsigned Ncall) {
     }();
     const unsigned gs = (Ncall <= 17 && !triples) ? 2 : 3;
     G.steps = gs == 2 ? 1 : 2;
+    G.f32_exact = Ncall <= 10 && !triples;
     unsigned j = 0;
     while (j < MP.N) {
         const unsigned e = j + gs < MP.N ? j + gs : MP.N;
@@ -451,14 +458,15 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
         emit(out + (size_t)j * plane, wr, wi);
     };
 
-    if constexpr (std::is_same<R, double>::value) {
+    // integer-valued f64 values -> group reductions -> planes
+    auto residues_f64 = [&](const double (&dr)[16], const double (&di)[16]) {
         for (int gi = 0; gi < G.ng; ++gi) {
             const double P = G.P[gi], rP = G.rP[gi];
             float tr[16], tim[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                tr[q] = __double2float_rn(__builtin_fma(__builtin_rint(yr[q] * rP), -P, yr[q]));
-                tim[q] = CPLX ? __double2float_rn(__builtin_fma(__builtin_rint(yi[q] * rP), -P, yi[q])) : 0.0f;
+                tr[q] = __double2float_rn(__builtin_fma(__builtin_rint(dr[q] * rP), -P, dr[q]));
+                tim[q] = CPLX ? __double2float_rn(__builtin_fma(__builtin_rint(di[q] * rP), -P, di[q])) : 0.0f;
             }
             if (G.steps == 1) {
                 for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from.template operator()<1>((unsigned)j, tr, tim);
@@ -466,8 +474,22 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                 for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from.template operator()<2>((unsigned)j, tr, tim);
             }
         }
+    };
+
+    if constexpr (std::is_same<R, double>::value) {
+        residues_f64(yr, yi);
+    } else if (G.f32_exact) {
+        // f32 operands whose residues mod_8i<float> computes exactly (G.f32_exact): the same
+        // residues through the f64 group form, a fraction of the f32 work
+        double dr[16], di[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            dr[q] = (double)yr[q];
+            di[q] = CPLX ? (double)yi[q] : 0.0;
+        }
+        residues_f64(dr, di);
     } else {
-        // f32 operands: mod_8i's four f32 steps per modulus (scaling.hpp:225-230)
+        // f32 operands, any N: mod_8i's four f32 steps per modulus (scaling.hpp:225-230)
         for (unsigned j = 0; j < MP.N; ++j) {
             const int p = MP.p[j];
             const float rf = MP.rinv_f[j];

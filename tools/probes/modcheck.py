@@ -45,3 +45,19 @@ for L in [53, 58, 60, 66, 70, 72, 73, 74, 76]:
             else:
                 bad += np.sum(got != exp)
         print(f"L={L} groups={g} steps={steps}: mismatches {bad}")
+
+# f32 operands: mod_8i<float>'s four f32 steps from x itself vs exact, for float-valued |x| < 2^L
+def f32_four_steps(x, p):
+    t = x.astype(np.float32)
+    for _ in range(4):
+        t = f32_step_fma(t, p)
+    return t.astype(np.int64)
+for L in [40, 44, 45, 46, 47, 48, 50]:
+    x = np.trunc(np.ldexp((rng.random(20000) * 2 - 1).astype(np.float32).astype(np.float64), L)).astype(np.float32)
+    xi = [int(v) for v in x.astype(np.float64)]
+    bad = 0
+    for p in P:
+        exp = np.array([((v + p // 2) % p) - p // 2 for v in xi])
+        got = f32_four_steps(x, p)
+        bad += np.sum((got & 255) != (exp & 255)) if p == 256 else np.sum(got != exp)
+    print(f"f32 four steps, L={L}: mismatches {bad}")
