@@ -126,7 +126,7 @@ static void phase_bound(const Call &c, const Views &v) {
     // the B tail defect lives in the op-N big-matrix extraction only (scaling.hpp:2312-2323, 3201-3203)
     split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.st,
                  c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE && c.B.contig);
-    (void)hipMemsetAsync(v.bound, 0, (L.m_pad + L.n_pad) * sizeof(int32_t), c.st);
+    zero_i32(v.bound, L.m_pad + L.n_pad, c.st);
     gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
 }
 
@@ -322,7 +322,7 @@ int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, si
     if (m == 0 && n == 0) return GEMMUL8_OK;
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, c.cplx);
     if (m == 0 || n == 0) {  // an empty block contributes nothing to the other operand's maxima
-        (void)hipMemsetAsync(v.bound, 0, (v.L.m_pad + v.L.n_pad) * sizeof(int32_t), c.st);
+        oz2::zero_i32(v.bound, v.L.m_pad + v.L.n_pad, c.st);
         return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
     }
     oz2::phase_bound(c, v);

@@ -29,6 +29,8 @@ void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, cons
 // cplx_rows: complex A bound of row v = max(bound[v], bound[v + nvec]) (scaling.hpp:2561-2588)
 void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
                              hipStream_t st, bool cplx_rows = false);
+// p[0, n) = 0 on the stream (graph-capturable)
+void zero_i32(int32_t *p, size_t n, hipStream_t st);
 
 // ---- gemm_i8.hip ----
 enum class Epi : int { RESIDUE = 0, BOUND = 1, RAW = 2 };

@@ -526,6 +526,18 @@ __global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, c
     sft_out[v] = (int16_t)(-s);
 }
 
+// zeroes the accurate-mode bound maxima before the bound product (a kernel rather than
+// hipMemsetAsync: a memset captured into a HIP graph did not run on replay -- the replayed
+// atomicMax then kept the previous call's maxima, tests/test_gpu_streams.py)
+__global__ void zero_i32_kernel(int32_t *__restrict__ p, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = 0;
+}
+void zero_i32(int32_t *p, size_t n, hipStream_t st) {
+    if (n == 0) return;
+    const size_t blocks = (n + 255) / 256;
+    zero_i32_kernel<<<dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st>>>(p, n);
+}
+
 // ------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------

@@ -1,0 +1,111 @@
+"""Stream semantics of the drop-in call (SURVEY.md 8(b) "Threading and streams"): the reference
+runs every kernel on the null stream with hipDeviceSynchronize around each phase
+(gemmul8.cu:251-289) and keeps its launch configuration in globals (common.hpp:11-20), so it can
+neither be captured into a graph nor called from two threads at once.  This build runs every
+kernel on the caller's stream with no device-wide synchronisation and per-call state only; these
+tests hold it to that:
+  * a call captured into a HIP graph and replayed gives the same bits as a direct call
+    (nothing in the call path allocates, synchronises or reads back);
+  * two host threads calling on two streams at once, each with its own workspace, give the same
+    bits as the calls one after the other."""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+class _Lazy:  # the library is imported on first use (CPU collection does not load it)
+    def __getattr__(self, name):
+        import gemmul8
+        return getattr(gemmul8, name)
+
+
+G = _Lazy()
+
+
+def _same(a, b):
+    return a.shape == b.shape and torch.equal(a.contiguous().view(torch.uint8), b.contiguous().view(torch.uint8))
+
+
+def _inputs(m, n, k, seed, dtype=torch.float64):
+    A = G.randmat(m, k, dtype, 0.5, seed)
+    B = G.randmat(k, n, dtype, 0.5, seed + 1)
+    return A, B
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_graph_capture_replay_same_bits(fast):
+    m, n, k, N = 300, 260, 513, 14
+    A, B = _inputs(m, n, k, 11)
+    W = G.alloc_work(m, n, k, N)
+    C_ref = torch.zeros((n, m), dtype=torch.float64, device="cuda")
+    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C_ref, m, N, fast, W)
+    torch.cuda.synchronize()
+
+    C = torch.zeros_like(C_ref)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, W, stream=s)
+    torch.cuda.synchronize()
+    C.zero_()
+    W.zero_()  # the replay must rebuild everything it reads from the workspace
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert _same(C, C_ref)
+
+    # replay picks up new operand values written into the captured buffers
+    A2, B2 = _inputs(m, n, k, 99)
+    A.copy_(A2)
+    B.copy_(B2)
+    g.replay()
+    C2_ref = torch.zeros_like(C_ref)
+    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A2, m, B2, k, 0.0, C2_ref, m, N, fast, G.alloc_work(m, n, k, N))
+    torch.cuda.synchronize()
+    assert _same(C, C2_ref)
+
+
+def test_two_threads_two_streams_same_bits():
+    shapes = [(520, 384, 700, 14, True, torch.float64), (256, 640, 1100, 9, False, torch.float32)]
+    jobs = []
+    for i, (m, n, k, N, fast, dt) in enumerate(shapes):
+        A, B = _inputs(m, n, k, 100 + i, dt)
+        jobs.append(dict(m=m, n=n, k=k, N=N, fast=fast, A=A, B=B, W=G.alloc_work(m, n, k, N),
+                         C=torch.zeros((n, m), dtype=dt, device="cuda"), ref=None))
+    for j in jobs:  # one after the other on the default stream
+        C = torch.zeros_like(j["C"])
+        G.gemm(G.OP_N, G.OP_N, j["m"], j["n"], j["k"], 1.0, j["A"], j["m"], j["B"], j["k"], 0.0, C, j["m"], j["N"],
+               j["fast"], j["W"])
+        j["ref"] = C
+    torch.cuda.synchronize()
+
+    errors = []
+    barrier = threading.Barrier(len(jobs))
+
+    def worker(j):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                barrier.wait()
+                for _ in range(5):
+                    G.gemm(G.OP_N, G.OP_N, j["m"], j["n"], j["k"], 1.0, j["A"], j["m"], j["B"], j["k"], 0.0, j["C"],
+                           j["m"], j["N"], j["fast"], j["W"], stream=s)
+                s.synchronize()
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(j,)) for j in jobs]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    for j in jobs:
+        assert _same(j["C"], j["ref"])
+    assert np.isfinite(jobs[0]["C"].cpu().numpy()).all()
