@@ -36,22 +36,33 @@ def _inputs(m, n, k, seed, dtype=torch.float64):
     return A, B
 
 
-@pytest.mark.parametrize("fast", [True, False])
-def test_graph_capture_replay_same_bits(fast):
-    m, n, k, N = 300, 260, 513, 14
-    A, B = _inputs(m, n, k, 11)
-    W = G.alloc_work(m, n, k, N)
-    C_ref = torch.zeros((n, m), dtype=torch.float64, device="cuda")
-    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C_ref, m, N, fast, W)
-    torch.cuda.synchronize()
+@pytest.mark.parametrize("dtype,ctype,fast,S", [
+    (torch.float64, 0, True, None),
+    (torch.float64, 0, False, None),
+    (torch.float32, 0, False, None),
+    (torch.complex128, 1, False, None),   # COMPLEX_BIG_MATRIX_ENCODE, accurate (bound of 2m rows)
+    (torch.complex128, 3, True, None),    # COMPLEX_KARATSUBA_MULT
+    (torch.float64, 0, False, 4),         # low-memory mode: moduli in groups of 4
+])
+def test_graph_capture_replay_same_bits(dtype, ctype, fast, S):
+    m, n, k, N = 300, 260, 513, 14 if ctype == 0 else 7
+    A, B = _inputs(m, n, k, 11, dtype)
+    W = G.alloc_work(m, n, k, N, ctype, slice_planes=S)
 
+    def direct(A, B, W):
+        C = torch.zeros((n, m), dtype=dtype, device="cuda")
+        G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, W, ctype, slice_planes=S)
+        torch.cuda.synchronize()
+        return C
+
+    C_ref = direct(A, B, W)
     C = torch.zeros_like(C_ref)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
     with torch.cuda.stream(s):
         with torch.cuda.graph(g, stream=s):
-            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, W, stream=s)
+            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, W, ctype, stream=s, slice_planes=S)
     torch.cuda.synchronize()
     C.zero_()
     W.zero_()  # the replay must rebuild everything it reads from the workspace
@@ -60,15 +71,14 @@ def test_graph_capture_replay_same_bits(fast):
     torch.cuda.synchronize()
     assert _same(C, C_ref)
 
-    # replay picks up new operand values written into the captured buffers
-    A2, B2 = _inputs(m, n, k, 99)
+    # replay picks up new operand values written into the captured buffers (accurate mode: the
+    # bound maxima of the previous replay must not survive)
+    A2, B2 = _inputs(m, n, k, 99, dtype)
     A.copy_(A2)
     B.copy_(B2)
     g.replay()
-    C2_ref = torch.zeros_like(C_ref)
-    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A2, m, B2, k, 0.0, C2_ref, m, N, fast, G.alloc_work(m, n, k, N))
     torch.cuda.synchronize()
-    assert _same(C, C2_ref)
+    assert _same(C, direct(A2, B2, G.alloc_work(m, n, k, N, ctype, slice_planes=S)))
 
 
 def test_two_threads_two_streams_same_bits():
