@@ -1,14 +1,19 @@
 // gemmul8.hip -- orchestration, the drop-in C++ API (include/gemmul8.hpp) and the C ABI
 // (include/gemmul8_c.h) of the MI355X Ozaki-scheme-II emulator.
 //
-// Per call, on ONE stream and with no device-wide synchronisation:
-//   fast mode      stats(A), stats(B) -> encode(A), encode(B)            split.hip
+// Per call, on the caller's stream and with no device-wide synchronisation:
+//   fast mode      stats(A) -> encode(A)  ||  stats(B) -> encode(B)       split.hip
 //   accurate mode  amax(A,B) -> 6-bit magnitudes -> bound product -> shifts -> encode
 //   products       one launch, all moduli, fused mod-p epilogue         gemm_i8.hip
 //   recombination  CRT + scaling + alpha/beta                           crt.hip
 // The reference runs the same phases with 4N+4 hipDeviceSynchronize calls, a
 // per-modulus hipblasGemmEx and a separate conversion kernel (gemmul8.cu:149-723).
+// Operand B's split runs on a second stream ("lane") forked from and joined back into the
+// caller's stream by events, so the two operands' split kernels overlap where either one alone
+// leaves the chip idle (small or strided operands); the join precedes everything that reads
+// both.  Events only: the call stays asynchronous and graph-capturable.
 #include <cstdio>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -33,7 +38,89 @@ struct Call {
     void *work;
     int VT;
     hipStream_t st;
+    hipStream_t stB;  // operand B's split work: the lane's stream, or st without a lane
+    struct Lane *lane;
 };
+
+// ---------------- operand-B lane: a second stream with fork / join events ----------------
+struct Lane {
+    hipStream_t s;
+    hipEvent_t fork, join;
+    int dev;
+};
+namespace lanes {
+static std::mutex mu;
+static std::vector<Lane *> free_list;
+static bool disabled() {  // GEMMUL8_SINGLE_STREAM=1: everything on the caller's stream (A-B runs)
+    static const bool d = [] {
+        const char *e = getenv("GEMMUL8_SINGLE_STREAM");
+        return e && atoi(e) != 0;
+    }();
+    return d;
+}
+static Lane *acquire(hipStream_t st) {
+    if (disabled()) return nullptr;
+    int dev = 0;
+    if (hipStreamGetDevice(st, &dev) != hipSuccess) return nullptr;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        for (size_t i = 0; i < free_list.size(); ++i)
+            if (free_list[i]->dev == dev) {
+                Lane *l = free_list[i];
+                free_list[i] = free_list.back();
+                free_list.pop_back();
+                return l;
+            }
+    }
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+    if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
+    Lane *l = new Lane{nullptr, nullptr, nullptr, dev};
+    const bool ok = hipStreamCreateWithFlags(&l->s, hipStreamNonBlocking) == hipSuccess &&
+                    hipEventCreateWithFlags(&l->fork, hipEventDisableTiming) == hipSuccess &&
+                    hipEventCreateWithFlags(&l->join, hipEventDisableTiming) == hipSuccess;
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!ok) {  // no lane: the call runs on one stream
+        (void)hipGetLastError();
+        delete l;
+        return nullptr;
+    }
+    return l;
+}
+static void release(Lane *l) {
+    if (!l) return;
+    std::lock_guard<std::mutex> g(mu);
+    free_list.push_back(l);
+}
+}  // namespace lanes
+
+// holds a lane for the enqueue of one call (released once the join is enqueued: a later call
+// on the same lane queues behind this one's B work, which only orders, never races)
+struct LaneGuard {
+    Call &c;
+    explicit LaneGuard(Call &call) : c(call) {
+        // the fork / join costs ~10 us of stream latency: worth it from (m + n) k = 2^25 up
+        // (4096^3: split 0.228 -> 0.206 ms; 1024^3: 39 -> 50 us with the lane, so none there)
+        const bool big = (c.m + c.n) * c.k >= ((size_t)1 << 25);
+        c.lane = big ? lanes::acquire(c.st) : nullptr;
+        c.stB = c.lane ? c.lane->s : c.st;
+    }
+    ~LaneGuard() {
+        lanes::release(c.lane);
+        c.lane = nullptr;
+        c.stB = c.st;
+    }
+};
+static void fork(const Call &c) {
+    if (!c.lane) return;
+    (void)hipEventRecord(c.lane->fork, c.st);
+    (void)hipStreamWaitEvent(c.stB, c.lane->fork, 0);
+}
+static void join(const Call &c) {
+    if (!c.lane) return;
+    (void)hipEventRecord(c.lane->join, c.stB);
+    (void)hipStreamWaitEvent(c.st, c.lane->join, 0);
+}
 
 // ---------------- phase timing (HIP events on the call's stream) ----------------
 namespace timing {
@@ -115,49 +202,58 @@ static ModParams sub_mod_params(unsigned N, unsigned j0, unsigned j1) {
 }
 
 // accurate mode, first half of phase 1: sft0 = 5 - ilogb(amax), the 6-bit magnitude planes and the
-// bound product's row / column maxima (scaling.hpp:3053-3100)
+// bound product's row / column maxima (scaling.hpp:3053-3100).  A on the call's stream, B on the lane.
 static void phase_bound(const Call &c, const Views &v) {
     const Layout &L = v.L;
     const ModParams MP = make_mod_params(c.N);
+    fork(c);
     split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
-    split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.st);
     split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
+    split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.stB);
     // big-matrix B magnitudes carry the reference's tail defect; classic / Karatsuba do not
     // the B tail defect lives in the op-N big-matrix extraction only (scaling.hpp:2312-2323, 3201-3203)
-    split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.st,
+    split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.stB,
                  c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE && c.B.contig);
+    join(c);
     zero_i32(v.bound, L.m_pad + L.n_pad, c.st);
     gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
 }
 
-// phase 1a: shifts of every row of op(A) / column of op(B), shared by all moduli
-// (scaling.hpp:3680-3734 fast, :3053-3136 accurate).  bound_ready: accurate mode takes the row /
-// column maxima already in the workspace (phase_bound, possibly combined across row blocks).
-static void phase_shifts(const Call &c, const Views &v, bool bound_ready) {
+// phase 1a: shifts of every row of op(A) (is_A) or column of op(B), shared by all moduli
+// (scaling.hpp:3680-3734 fast, :3053-3136 accurate: from the bound maxima already in the workspace)
+static void operand_shifts(const Call &c, const Views &v, bool is_A, hipStream_t st) {
     const Layout &L = v.L;
     if (c.fast) {
         const float log2M = oz2_log2M_fast[c.N - 2];
-        split_stats(c.A, c.k, c.m, c.VT, false, log2M, v.sftA, c.st);
-        split_stats(c.B, c.k, c.n, c.VT, false, log2M, v.sftB, c.st);
+        if (is_A) split_stats(c.A, c.k, c.m, c.VT, false, log2M, v.sftA, st);
+        else split_stats(c.B, c.k, c.n, c.VT, false, log2M, v.sftB, st);
     } else {
         const float log2M = oz2_log2M_accu[c.N - 2];
-        if (!bound_ready) phase_bound(c, v);
-        split_finalize_accurate(v.sft0, v.bound, c.m, log2M, v.sftA, c.st, c.cplx);
-        split_finalize_accurate(v.sft0 + L.m_pad, v.bound + L.m_pad, c.n, log2M, v.sftB, c.st);
+        if (is_A) split_finalize_accurate(v.sft0, v.bound, c.m, log2M, v.sftA, st, c.cplx);
+        else split_finalize_accurate(v.sft0 + L.m_pad, v.bound + L.m_pad, c.n, log2M, v.sftB, st);
     }
 }
 
-// phase 1b: slices of moduli [j0, j1) into the slice planes starting at `slot`
-static void phase_encode(const Call &c, const Views &v, unsigned j0, unsigned j1, unsigned slot) {
+// phase 1b: slices of moduli [j0, j1) of one operand into the slice planes starting at `slot`
+static void operand_encode(const Call &c, const Views &v, bool is_A, unsigned j0, unsigned j1, unsigned slot,
+                           hipStream_t st) {
     const Layout &L = v.L;
     const ModParams SP = sub_mod_params(c.N, j0, j1);
-    split_encode(c.A, true, c.m, c.k, v.sftA, v.A8 + slot * L.planeA, L.planeA, L, 0, SP, c.st);
-    split_encode(c.B, false, c.n, c.k, v.sftB, v.B8 + slot * L.planeB, L.planeB, L, 0, SP, c.st);
+    if (is_A) split_encode(c.A, true, c.m, c.k, v.sftA, v.A8 + slot * L.planeA, L.planeA, L, 0, SP, st);
+    else split_encode(c.B, false, c.n, c.k, v.sftB, v.B8 + slot * L.planeB, L.planeB, L, 0, SP, st);
 }
 
+// phase 1 (shifts + slices of moduli [j0, j1) into their own planes); bound_ready: accurate mode
+// takes the row / column maxima already in the workspace (phase_bound, possibly combined across
+// row blocks)
 static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1, bool bound_ready) {
-    phase_shifts(c, v, bound_ready);
-    phase_encode(c, v, j0, j1, j0);
+    if (!c.fast && !bound_ready) phase_bound(c, v);
+    fork(c);
+    operand_shifts(c, v, true, c.st);
+    operand_encode(c, v, true, j0, j1, j0, c.st);
+    operand_shifts(c, v, false, c.stB);
+    operand_encode(c, v, false, j0, j1, j0, c.stB);
+    join(c);
 }
 
 // phase 2: residue planes j0..j1-1 from the slice planes starting at `slot` (one launch;
@@ -175,8 +271,9 @@ static void phase_crt(const Views &v, unsigned N, OutType ot, const void *alpha,
     crt_inverse(v.R, v.L, v.sftA, v.sftB, CP, ot, alpha, beta, C, ldc, st);
 }
 
-static int run(const Call &c, double *phase_ns) {
+static int run(Call &c, double *phase_ns) {
     const Views v = views(c.work, c.m, c.n, c.k, c.N, c.cplx, c.slice_planes);
+    LaneGuard lane(c);
 
     const bool want_events = phase_ns != nullptr;
     bool record;
@@ -196,11 +293,18 @@ static int run(const Call &c, double *phase_ns) {
     } else {
         // low-memory mode: the moduli in groups of S through the same S slice planes (each group
         // re-reads A and B); the product phase timer then includes the re-encoding
-        phase_shifts(c, v, false);
+        if (!c.fast) phase_bound(c, v);
+        fork(c);
+        operand_shifts(c, v, true, c.st);
+        operand_shifts(c, v, false, c.stB);
+        join(c);
         if (record) (void)hipEventRecord(rec.ev[0], c.st);
         for (unsigned j0 = 0; j0 < c.N; j0 += S) {
             const unsigned j1 = j0 + S < c.N ? j0 + S : c.N;
-            phase_encode(c, v, j0, j1, 0);
+            fork(c);
+            operand_encode(c, v, true, j0, j1, 0, c.st);
+            operand_encode(c, v, false, j0, j1, 0, c.stB);
+            join(c);
             phase_products(v, c.N, j0, j1, 0, c.st);
         }
     }
@@ -268,6 +372,8 @@ static int prepare(void *stream, int op_a, int op_b, size_t m, size_t n, size_t 
     // 512 for gemm<float>, 128 for gemm<double>, the mixed and the complex paths
     c.VT = (ta == GEMMUL8_R_32F && tb == GEMMUL8_R_32F && tc == GEMMUL8_R_32F) ? 512 : 128;
     c.st = static_cast<hipStream_t>(stream);
+    c.stB = c.st;
+    c.lane = nullptr;
     return GEMMUL8_OK;
 }
 
@@ -325,6 +431,7 @@ int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, si
         oz2::zero_i32(v.bound, v.L.m_pad + v.L.n_pad, c.st);
         return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
     }
+    oz2::LaneGuard lane(c);
     oz2::phase_bound(c, v);
     return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
@@ -338,6 +445,7 @@ int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k
     if (rc != GEMMUL8_OK) return rc;
     if (mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
     if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::LaneGuard lane(c);
     oz2::phase_split(c, oz2::views(work, m, n, k, num_moduli, c.cplx), mod_begin, mod_end,
                      (flags & GEMMUL8_SPLIT_BOUND_READY) != 0);
     return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;

@@ -36,16 +36,20 @@ def _inputs(m, n, k, seed, dtype=torch.float64):
     return A, B
 
 
-@pytest.mark.parametrize("dtype,ctype,fast,S", [
-    (torch.float64, 0, True, None),
-    (torch.float64, 0, False, None),
-    (torch.float32, 0, False, None),
-    (torch.complex128, 1, False, None),   # COMPLEX_BIG_MATRIX_ENCODE, accurate (bound of 2m rows)
-    (torch.complex128, 3, True, None),    # COMPLEX_KARATSUBA_MULT
-    (torch.float64, 0, False, 4),         # low-memory mode: moduli in groups of 4
+@pytest.mark.parametrize("dtype,ctype,fast,S,big", [
+    (torch.float64, 0, True, None, False),
+    (torch.float64, 0, False, None, False),
+    (torch.float32, 0, False, None, False),
+    (torch.complex128, 1, False, None, False),   # COMPLEX_BIG_MATRIX_ENCODE, accurate (bound of 2m rows)
+    (torch.complex128, 3, True, None, False),    # COMPLEX_KARATSUBA_MULT
+    (torch.float64, 0, False, 4, False),         # low-memory mode: moduli in groups of 4
+    # (m + n) k >= 2^25: operand B's split runs on the second stream (fork / join in the graph)
+    (torch.float64, 0, True, None, True),
+    (torch.float64, 0, False, None, True),
+    (torch.float64, 0, False, 4, True),
 ])
-def test_graph_capture_replay_same_bits(dtype, ctype, fast, S):
-    m, n, k, N = 300, 260, 513, 14 if ctype == 0 else 7
+def test_graph_capture_replay_same_bits(dtype, ctype, fast, S, big):
+    m, n, k, N = (2048, 2040, 8192, 14) if big else (300, 260, 513, 14 if ctype == 0 else 7)
     A, B = _inputs(m, n, k, 11, dtype)
     W = G.alloc_work(m, n, k, N, ctype, slice_planes=S)
 
@@ -82,7 +86,8 @@ def test_graph_capture_replay_same_bits(dtype, ctype, fast, S):
 
 
 def test_two_threads_two_streams_same_bits():
-    shapes = [(520, 384, 700, 14, True, torch.float64), (256, 640, 1100, 9, False, torch.float32)]
+    shapes = [(520, 384, 700, 14, True, torch.float64), (256, 640, 1100, 9, False, torch.float32),
+              (2048, 2048, 8192, 12, False, torch.float64), (1800, 2300, 8000, 14, True, torch.float64)]
     jobs = []
     for i, (m, n, k, N, fast, dt) in enumerate(shapes):
         A, B = _inputs(m, n, k, 100 + i, dt)
