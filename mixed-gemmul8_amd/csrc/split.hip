@@ -46,6 +46,7 @@ struct ModGroups {
     int ng;
     int steps;      // f32 steps per modulus (1: pairs, 2: triples)
     int f32_exact;  // f32 operands: mod_8i<float>'s four f32 steps are exact (N <= 10), so the f64 form applies
+    int bytes;      // pair form straight to bytes (plane_bytes); GEMMUL8_ENC_BYTES=0 keeps the convert-and-pack form
     int start[OZ2_MAX_MODULI + 1];
     double P[OZ2_MAX_MODULI];
     double rP[OZ2_MAX_MODULI];
@@ -59,6 +60,11 @@ static ModGroups make_groups(const ModParams &MP, unsigned Ncall) {
     const unsigned gs = (Ncall <= 17 && !triples) ? 2 : 3;
     G.steps = gs == 2 ? 1 : 2;
     G.f32_exact = Ncall <= 10 && !triples;
+    static const bool no_bytes = [] {
+        const char *e = getenv("GEMMUL8_ENC_BYTES");
+        return e && atoi(e) == 0;
+    }();
+    G.bytes = !no_bytes;
     unsigned j = 0;
     while (j < MP.N) {
         const unsigned e = j + gs < MP.N ? j + gs : MP.N;
@@ -458,6 +464,48 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
         emit(out + (size_t)j * plane, wr, wi);
     };
 
+    // Pair form (one f32 step per modulus) straight to bytes.  With C = 1.5*2^23 and tc = t + C
+    // (exact, |t| < 2^22): y' = fma(t, fl(1/p), C) rounds t*fl(1/p) to an integer once (values in
+    // [2^23, 2^24) have ulp 1), and fma(y' - C, -p, tc) = C + (t - rint(t/p)*p) exactly, whose bit
+    // pattern carries the residue in its low byte (two's complement, as the int8 cast of mod_8i
+    // stores it).  Three packed ops per pair and three byte permutes per four bytes replace the
+    // multiply / round / fma, the f32 -> i32 conversion and the shift-or packing.
+    auto plane_bytes = [&](unsigned j, const float (&tr)[16], const float (&trc)[16], const float (&ti)[16],
+                           const float (&tic)[16]) {
+        const float rf = MP.rinv_f[j];
+        const f2v C2 = {12582912.0f, 12582912.0f}, r2 = {rf, rf}, q2 = {-(float)MP.p[j], -(float)MP.p[j]};
+        uint32_t br[16], bi[16];
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+            f2v y = __builtin_elementwise_fma(f2v{tr[q], tr[q + 1]}, r2, C2) - C2;
+            const f2v a = __builtin_elementwise_fma(y, q2, f2v{trc[q], trc[q + 1]});
+            br[q] = __float_as_uint(a.x);
+            br[q + 1] = __float_as_uint(a.y);
+            if (CPLX) {
+                y = __builtin_elementwise_fma(f2v{ti[q], ti[q + 1]}, r2, C2) - C2;
+                const f2v b = __builtin_elementwise_fma(y, q2, f2v{tic[q], tic[q + 1]});
+                bi[q] = __float_as_uint(b.x);
+                bi[q + 1] = __float_as_uint(b.y);
+            }
+        }
+        uint32_t wr[4], wi[4];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            // low bytes of four words -> one word (v_perm_b32: selectors 0-3 pick the second source)
+            const uint32_t lo = __builtin_amdgcn_perm(br[4 * d + 1], br[4 * d], 0x0c0c0400u);
+            const uint32_t hi = __builtin_amdgcn_perm(br[4 * d + 3], br[4 * d + 2], 0x0c0c0400u);
+            wr[d] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            if (CPLX) {
+                const uint32_t l2 = __builtin_amdgcn_perm(bi[4 * d + 1], bi[4 * d], 0x0c0c0400u);
+                const uint32_t h2 = __builtin_amdgcn_perm(bi[4 * d + 3], bi[4 * d + 2], 0x0c0c0400u);
+                wi[d] = __builtin_amdgcn_perm(h2, l2, 0x05040100u);
+            } else {
+                wi[d] = 0;
+            }
+        }
+        emit(out + (size_t)j * plane, wr, wi);
+    };
+
     // integer-valued f64 values -> group reductions -> planes
     auto residues_f64 = [&](const double (&dr)[16], const double (&di)[16]) {
         for (int gi = 0; gi < G.ng; ++gi) {
@@ -468,7 +516,15 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                 tr[q] = __double2float_rn(__builtin_fma(__builtin_rint(dr[q] * rP), -P, dr[q]));
                 tim[q] = CPLX ? __double2float_rn(__builtin_fma(__builtin_rint(di[q] * rP), -P, di[q])) : 0.0f;
             }
-            if (G.steps == 1) {
+            if (G.steps == 1 && G.bytes && OZ2_ENC_ABLATE == 0) {
+                float trc[16], tic[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    trc[q] = tr[q] + 12582912.0f;
+                    tic[q] = tim[q] + 12582912.0f;
+                }
+                for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_bytes((unsigned)j, tr, trc, tim, tic);
+            } else if (G.steps == 1) {
                 for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from.template operator()<1>((unsigned)j, tr, tim);
             } else {
                 for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from.template operator()<2>((unsigned)j, tr, tim);
