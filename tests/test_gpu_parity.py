@@ -322,3 +322,22 @@ def test_residue_epilogue_exhaustive(path):
     assert G.lib.gemmul8_residue_selftest(G._stream(), path) == 0
     if path == 0:  # negative control: a wrong expectation is counted for every (input, modulus) pair
         assert G.lib.gemmul8_residue_selftest(G._stream(), 2) == ((1 << 31) + 1) * 20
+
+
+@pytest.mark.parametrize("N", [10, 11, 17, 18])
+@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_encode_form_boundaries(N, fast, dt):
+    """The encode switches residue forms by N (split.hip ModGroups): f64 pairs with one f32 step
+    straight to bytes for N <= 17, triples with two steps above; f32 operands through the f64
+    form for N <= 10 and mod_8i<float>'s four f32 steps above.  Wide dynamic range (phi = 3) and a
+    row / column whose maximum dwarfs the rest put scaled values at the top of the magnitude range."""
+    rng = np.random.default_rng(900 + N + 50 * fast + (dt == np.float32))
+    m, n, k = 150, 130, 300
+    A = randmat_np(rng, m, k, phi=3.0, dtype=dt)
+    B = randmat_np(rng, k, n, phi=3.0, dtype=dt)
+    A[5, :] *= dt(1e-6)
+    A[5, 17] = dt(3.0e4)
+    B[:, 9] *= dt(1e-5)
+    B[200, 9] = dt(-7.0e3)
+    check_full(A, B, N, fast=fast)
