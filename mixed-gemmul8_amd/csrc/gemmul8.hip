@@ -72,6 +72,9 @@ static Lane *acquire(hipStream_t st) {
                 return l;
             }
     }
+    // no new streams or events while the caller captures a graph (the call then runs on one stream)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) return nullptr;
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
@@ -164,6 +167,10 @@ static void resolve_all() {
 }  // namespace timing
 
 static inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
+static bool is_capturing(hipStream_t st) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
+}
 
 // Workspace views of one call (layout: oz2_common.hpp make_layout)
 struct Views {
@@ -275,12 +282,17 @@ static int run(Call &c, double *phase_ns) {
     const Views v = views(c.work, c.m, c.n, c.k, c.N, c.cplx, c.slice_planes);
     LaneGuard lane(c);
 
-    const bool want_events = phase_ns != nullptr;
+    // a call being captured into a graph records no timing events and returns zero phase times
+    // (reading them back would synchronise inside the capture)
+    const bool capturing = is_capturing(c.st);
+    if (phase_ns && capturing)
+        for (int i = 0; i < 4; ++i) phase_ns[i] = 0.0;
+    const bool want_events = phase_ns != nullptr && !capturing;
     bool record;
     timing::Rec rec{};
     {
         std::lock_guard<std::mutex> g(timing::mu);
-        record = want_events || timing::enabled;
+        record = want_events || (timing::enabled && !capturing);
         if (record) rec = timing::acquire();
     }
     if (record) (void)hipEventRecord(rec.start, c.st);
@@ -463,7 +475,7 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
     oz2::timing::Rec rec{};
     {
         std::lock_guard<std::mutex> g(oz2::timing::mu);
-        record = oz2::timing::enabled;
+        record = oz2::timing::enabled && !oz2::is_capturing(st);
         if (record) rec = oz2::timing::acquire();
     }
     if (record) {

@@ -109,6 +109,27 @@ int main() {
         CHECK(hipMemcpy(raw.data(), Zc, raw.size(), hipMemcpyDeviceToHost) == hipSuccess);
         for (unsigned char c : raw) CHECK(c == 0x3c);
     }
+    // the C++ API inside a HIP graph capture on the handle's stream: zero phase times (no readback
+    // inside the capture), and the instantiated graph reproduces the direct call's bits
+    for (int fast = 1; fast >= 0; --fast) {
+        CHECK(hipMemset(C, 0, m * n * sizeof(double)) == hipSuccess);
+        CHECK(hipDeviceSynchronize() == hipSuccess);
+        hipGraph_t g;
+        hipGraphExec_t ge;
+        CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeGlobal) == hipSuccess);
+        std::vector<double> t = gemmul8::gemm<double>(h, HIPBLAS_OP_N, HIPBLAS_OP_N, m, n, k, &one, A, m, B, k, &zero, C,
+                                                      m, N, fast != 0, work);
+        CHECK(hipStreamEndCapture(st, &g) == hipSuccess);
+        CHECK(t == std::vector<double>(4, 0.0));
+        CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) == hipSuccess);
+        CHECK(hipGraphLaunch(ge, st) == hipSuccess);
+        CHECK(gemmul8_gemm(st, GEMMUL8_OP_N, GEMMUL8_OP_N, m, n, k, GEMMUL8_R_64F, GEMMUL8_R_64F, GEMMUL8_R_64F, &one, A,
+                           m, B, k, &zero, C2, m, N, fast, work, GEMMUL8_REAL_DEFAULT, nullptr) == GEMMUL8_OK);
+        CHECK(hipStreamSynchronize(st) == hipSuccess);
+        CHECK(download(C, m * n) == download(C2, m * n));
+        CHECK(hipGraphExecDestroy(ge) == hipSuccess);
+        CHECK(hipGraphDestroy(g) == hipSuccess);
+    }
     std::printf("OK\n");
     return 0;
 }

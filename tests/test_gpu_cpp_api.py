@@ -1,7 +1,8 @@
 """GPU: the reference's C++ API (include/gemmul8.hpp: workSize + gemm<TA,TB,TC> with a hipBLAS
 handle) used from C++ exactly as code written for the reference would use it (tests/cpp/api_check.cpp,
 compiled here with hipcc and linked against libgemmul8_amd.so): bit-identical to the C ABI, the
-handle's stream honoured, invalid compute types rejected with {0,0,0,0}."""
+handle's stream honoured, invalid compute types rejected with {0,0,0,0}, and a call captured into a
+HIP graph on the handle's stream replays bit-identically."""
 import os
 import subprocess
 
