@@ -50,6 +50,7 @@ struct Api {
     hipError_t (*malloc_)(void **, size_t) = nullptr;
     decltype(&hipFree) free_ = nullptr;
     decltype(&hipStreamSynchronize) streamSync = nullptr;
+    decltype(&hipStreamIsCapturing) isCapturing = nullptr;
     decltype(&hipblasGetStream) hbGetStream = nullptr;
     decltype(&hipblasGetPointerMode) hbGetPointerMode = nullptr;
     decltype(&rocblas_get_stream) rbGetStream = nullptr;
@@ -73,6 +74,7 @@ struct Api {
         malloc_ = reinterpret_cast<decltype(malloc_)>(sym(hip, "hipMalloc"));
         free_ = reinterpret_cast<decltype(free_)>(sym(hip, "hipFree"));
         streamSync = reinterpret_cast<decltype(streamSync)>(sym(hip, "hipStreamSynchronize"));
+        isCapturing = reinterpret_cast<decltype(isCapturing)>(sym(hip, "hipStreamIsCapturing"));
         hbGetStream = reinterpret_cast<decltype(hbGetStream)>(sym(hipblas, "hipblasGetStream"));
         hbGetPointerMode = reinterpret_cast<decltype(hbGetPointerMode)>(sym(hipblas, "hipblasGetPointerMode"));
         rbGetStream = reinterpret_cast<decltype(rbGetStream)>(sym(rocblas, "rocblas_get_stream"));
@@ -165,6 +167,10 @@ void *workspace(size_t bytes, hipStream_t st) {
     std::lock_guard<std::mutex> g(mu);
     auto &e = pool[{dev, st}];
     if (e.second < bytes) {
+        // growing the workspace synchronises and allocates: not while the stream is captured into a
+        // graph (the call is forwarded to the vendor routine instead)
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (a.isCapturing && (a.isCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)) return nullptr;
         if (e.first) {
             (void)a.streamSync(st);
             (void)a.free_(e.first);

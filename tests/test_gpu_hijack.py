@@ -2,7 +2,8 @@
 PyTorch.  A child process loads libgemmul8_hijack.so into the global symbol scope before torch
 (the in-process equivalent of LD_PRELOAD), then calls torch.matmul: float64 / complex128
 products at or above the intercept thresholds must be the emulator's result bit for bit, smaller
-ones must reach the vendor routine."""
+ones must reach the vendor routine; under CUDA-graph capture the emulator runs where its workspace
+already exists and the call is forwarded where it would have to allocate."""
 import json
 import os
 import subprocess
@@ -37,6 +38,33 @@ Bb = torch.randn(3, 260, 280, dtype=torch.float64, device="cuda", generator=g)
 Cb = torch.bmm(Ab, Bb)                           # -> hipblasDgemmStridedBatched -> interposer
 Eb = torch.stack([G.matmul(Bb[i].t().contiguous(), Ab[i].t().contiguous(), 14).t() for i in range(3)])
 out["bmm_bits"] = bool(torch.equal(Cb, Eb))
+# under CUDA-graph capture: a stream whose workspace exists stays emulated inside the graph; a
+# stream without one is forwarded to the vendor routine (no allocation inside a capture)
+A = torch.randn(512, 448, dtype=torch.float64, device="cuda", generator=g)
+B = torch.randn(448, 384, dtype=torch.float64, device="cuda", generator=g)
+E = G.matmul(B.t().contiguous(), A.t().contiguous(), 14).t()
+s = torch.cuda.Stream()
+s.wait_stream(torch.cuda.current_stream())
+with torch.cuda.stream(s):
+    torch.matmul(A, B)                           # warms the workspace of stream s
+torch.cuda.synchronize()
+gr = torch.cuda.CUDAGraph()
+with torch.cuda.graph(gr, stream=s):
+    Cg = torch.matmul(A, B)
+gr.replay()
+torch.cuda.synchronize()
+out["graph_bits"] = bool(torch.equal(Cg, E))
+A2 = torch.randn(520, 450, dtype=torch.float64, device="cuda", generator=g)
+B2 = torch.randn(450, 390, dtype=torch.float64, device="cuda", generator=g)
+s2 = torch.cuda.Stream()
+s2.wait_stream(torch.cuda.current_stream())
+gr2 = torch.cuda.CUDAGraph()
+with torch.cuda.graph(gr2, stream=s2):
+    C2 = torch.matmul(A2, B2)
+gr2.replay()
+torch.cuda.synchronize()
+ex2 = A2.cpu() @ B2.cpu()
+out["graph_cold_relerr"] = float(((C2.cpu() - ex2).abs() / ex2.abs()).max())
 A = torch.randn(64, 64, dtype=torch.float64, device="cuda", generator=g)
 C = A @ A                                        # below the thresholds: forwarded
 out["small_relerr"] = float(((C - (A.cpu() @ A.cpu()).cuda()).abs().max() / (A.cpu() @ A.cpu()).abs().max()))
@@ -61,3 +89,6 @@ def test_torch_matmul_is_emulated():
     assert res["bmm_bits"], res
     assert res["d"]["relerr"] < 1e-9 and res["z"]["relerr"] < 1e-9, res
     assert res["small_relerr"] < 1e-12, res
+    assert res["graph_bits"], res
+    assert res["graph_cold_relerr"] < 1e-9, res
+    assert "m=390 n=520 k=450 -> emulated" not in log, log[-2000:]
