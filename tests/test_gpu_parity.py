@@ -341,3 +341,28 @@ def test_encode_form_boundaries(N, fast, dt):
     B[:, 9] *= dt(1e-5)
     B[200, 9] = dt(-7.0e3)
     check_full(A, B, N, fast=fast)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_offset_pointers(fast):
+    """A, B and C one element past an allocation's start (8-byte aligned only) and the workspace 16
+    bytes in (the reference assumes 16-byte alignment of `work`): same bits as aligned buffers"""
+    torch = _torch()
+    import gemmul8 as G
+    rng = np.random.default_rng(91 + fast)
+    m, n, k, N = 130, 70, 150, 14
+    A, B = randmat_np(rng, m, k), randmat_np(rng, k, n)
+    C_ref, _, _ = run_gpu(A, B, N, fast=fast)
+
+    def dev_offset(X):
+        flat = torch.zeros(X.size + 1, dtype=torch.float64, device="cuda")
+        flat[1:] = torch.from_numpy(np.asfortranarray(X).reshape(-1, order="F")).cuda()
+        return flat[1:]
+
+    dA, dB = dev_offset(A), dev_offset(B)
+    dC = dev_offset(np.zeros((m, n)))
+    wbuf = torch.empty(G.workSize(m, n, k, N) + 16, dtype=torch.uint8, device="cuda")
+    G.gemm(0, 0, m, n, k, 1.0, dA, m, dB, k, 0.0, dC, m, N, fast, wbuf[16:])
+    torch.cuda.synchronize()
+    Cg = dC.cpu().numpy().reshape((m, n), order="F")
+    assert np.asfortranarray(Cg).tobytes() == np.asfortranarray(C_ref).tobytes()
