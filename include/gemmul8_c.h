@@ -30,7 +30,7 @@ enum {
     GEMMUL8_E_MODULI = -1,       /* num_moduli outside [2, 20] */
     GEMMUL8_E_TYPES = -2,        /* unsupported dtype combination for compute_type */
     GEMMUL8_E_OP = -3,           /* unsupported transpose op */
-    GEMMUL8_E_SIZE = -4,         /* k beyond the int32-exact bound (2^17), or a leading dimension too small */
+    GEMMUL8_E_SIZE = -4,         /* padded k beyond 2^22 (fast) / 2^19 - 64 (accurate), or a leading dimension too small */
     GEMMUL8_E_UNSUPPORTED = -5,  /* compute type / mode not implemented on this build */
     GEMMUL8_E_HIP = -6           /* a HIP launch or runtime call failed */
 };

@@ -44,6 +44,8 @@ struct GemmArgs {
     const int8_t *B;
     size_t planeA, planeB;
     unsigned ksteps, mtiles, ntiles;
+    unsigned kstride, k0;            // panels per tile in the planes, first k-step of this launch
+    int accumulate;                  // RESIDUE: add this launch's residues into the planes mod p
     void *out;
     size_t planeOut, ldo;
     int32_t *rowmax, *colmax;
@@ -132,6 +134,17 @@ __device__ __forceinline__ uint32_t residue_biased(uint32_t u, uint32_t p, uint3
     const uint32_t q = __umulhi(u, m);
     const uint32_t r = u - __umul24(q, p);
     return min(r, r - p);
+}
+
+// four residues in [0, p) per word: (a + b) mod p bytewise
+__device__ __forceinline__ uint32_t add_mod_bytes(uint32_t a, uint32_t b, uint32_t p) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t s = ((a >> (8 * i)) & 0xffu) + ((b >> (8 * i)) & 0xffu);
+        r |= min(s, s - p) << (8 * i);
+    }
+    return r;
 }
 
 // One k-step of fragments for a wave: 4 row blocks of A, 2 column blocks of B, both 32-deep halves.
@@ -230,8 +243,14 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], i
             const uint4 v = *reinterpret_cast<const uint4 *>(lo + col * 64 + ((4 * qd) ^ (x & ~3)));
             const uint32_t e[4] = {v.x, v.y, v.z, v.w};
             const int pm = x & 3;
-            *reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd) =
-                make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+            uint4 *dst = reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd);
+            uint4 res = make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+            if (g.accumulate) {  // k-chunked product: (earlier chunks + this chunk) mod p, bytewise
+                const uint4 prev = *dst;
+                res = make_uint4(add_mod_bytes(res.x, prev.x, (uint32_t)p), add_mod_bytes(res.y, prev.y, (uint32_t)p),
+                                 add_mod_bytes(res.z, prev.z, (uint32_t)p), add_mod_bytes(res.w, prev.w, (uint32_t)p));
+            }
+            *dst = res;
         }
     } else if constexpr (EPI == (int)Epi::BOUND) {
         int32_t *rmax = reinterpret_cast<int32_t *>(smem);
@@ -305,14 +324,14 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     const unsigned tm = grp * GM + idx % gm, tn = idx / gm;
 
     // LDS-DMA pieces of this wave: 1 KiB blocks {wave, wave + 8} of the A and of the B panel
-    const int8_t *Ag = g.A + j * g.planeA + (size_t)tm * g.ksteps * PANEL + wave * 1024 + lane * 16;
-    const int8_t *Bg = g.B + j * g.planeB + (size_t)tn * g.ksteps * PANEL + wave * 1024 + lane * 16;
+    const int8_t *Ag = g.A + j * g.planeA + ((size_t)tm * g.kstride + g.k0) * PANEL + wave * 1024 + lane * 16;
+    const int8_t *Bg = g.B + j * g.planeB + ((size_t)tn * g.kstride + g.k0) * PANEL + wave * 1024 + lane * 16;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
     const uint32_t lds_wave = lds_base + wave * 1024;
     const v4si rA = make_rsrc(g.A + j * g.planeA, (uint32_t)g.planeA);
     const v4si rB = make_rsrc(g.B + j * g.planeB, (uint32_t)g.planeB);
-    const uint32_t oA = (uint32_t)((size_t)tm * g.ksteps * PANEL) + wave * 1024 + lane * 16;
-    const uint32_t oB = (uint32_t)((size_t)tn * g.ksteps * PANEL) + wave * 1024 + lane * 16;
+    const uint32_t oA = (uint32_t)(((size_t)tm * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
+    const uint32_t oB = (uint32_t)(((size_t)tn * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
     auto stage = [&](unsigned ks, unsigned slot) {
         const size_t go = (size_t)ks * PANEL;
         const uint32_t lo = lds_wave + slot * SLOT;
@@ -469,11 +488,32 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         g.minv[i] = (uint32_t)((((uint64_t)1) << 32) / p);
         g.bias[i] = (int)(((((uint64_t)1) << 30) + p - 1) / p * p);
     }
+    g.kstride = g.ksteps;
+    g.k0 = 0;
+    g.accumulate = 0;
     dim3 grid((unsigned)(L.mtiles * L.ntiles), nplanes);
     // GEMMUL8_FORCE_FLAT_DMA=1 takes the 64-bit path at any size (tests cover it with small shapes)
     const char *ff = getenv("GEMMUL8_FORCE_FLAT_DMA");
     const bool buf = L.planeA < ((size_t)1 << 32) && L.planeB < ((size_t)1 << 32) && !(ff && atoi(ff));
 #define OZ2_GEMM(E, B) gemm_i8_kernel<E, B><<<grid, dim3(NTHREADS), 0, st>>>(g)
+    // beyond k_pad = 2^17 an int32 product can wrap (the reference's int32 C32i does): the residue
+    // product then runs in k-chunks of 2^16 (biased path), each adding its residues into the planes
+    // mod p.  GEMMUL8_KCHUNK (k-steps, multiple of 1) forces chunking at small k for the tests.
+    static const unsigned forced_chunk = [] {
+        const char *e = getenv("GEMMUL8_KCHUNK");
+        return e ? (unsigned)atoi(e) : 0u;
+    }();
+    const unsigned chunk = forced_chunk ? forced_chunk : ((1u << 16) / KSTEP);
+    if (epi == Epi::RESIDUE && (L.k_pad > ((size_t)1 << 17) || (forced_chunk && g.ksteps > forced_chunk))) {
+        g.biased = 1;
+        for (unsigned k0 = 0; k0 < g.kstride; k0 += chunk) {
+            g.k0 = k0;
+            g.ksteps = g.kstride - k0 < chunk ? g.kstride - k0 : chunk;
+            g.accumulate = k0 > 0;
+            buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0);
+        }
+        return;
+    }
     switch (epi) {
     case Epi::RESIDUE: buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0); break;
     case Epi::BOUND: buf ? OZ2_GEMM(1, 1) : OZ2_GEMM(1, 0); break;

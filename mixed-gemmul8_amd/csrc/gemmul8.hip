@@ -369,7 +369,9 @@ static int prepare(void *stream, int op_a, int op_b, size_t m, size_t n, size_t 
     if (!cp && !(tc == GEMMUL8_R_64F || tc == GEMMUL8_R_32F)) return GEMMUL8_E_TYPES;
     if (op_a < 0 || op_a > 2 || op_b < 0 || op_b > 2) return GEMMUL8_E_OP;
     const size_t kr = cp ? 2 * round_up(k, KSTEP) : round_up(k, KSTEP);
-    if (kr > ((size_t)1 << 17)) return GEMMUL8_E_SIZE;
+    // fast mode: any k the encode grid spans (the residue product is k-chunked beyond 2^17, gemm_i8);
+    // accurate mode: the bound product of 6-bit magnitudes (|x| <= 2^12 k) must stay int32-exact
+    if (kr > (fast ? ((size_t)1 << 22) : (((size_t)1 << 19) - KSTEP))) return GEMMUL8_E_SIZE;
     const bool ta_t = op_a != GEMMUL8_OP_N, tb_t = op_b != GEMMUL8_OP_N;
     if (lda < (ta_t ? k : m) || ldb < (tb_t ? n : k) || ldc < m) return GEMMUL8_E_SIZE;
     c.A = OperandDesc{A, lda, ta_t, dt_dbl(ta), cp, cp && op_a == GEMMUL8_OP_C};

@@ -23,7 +23,7 @@ OP_N, OP_T, OP_C = 0, 1, 2
 R_64F, R_32F, C_64F, C_32F = 0, 1, 2, 3
 _DTYPE = {torch.float64: R_64F, torch.float32: R_32F, torch.complex128: C_64F, torch.complex64: C_32F}
 _ERR = {-1: "num_moduli outside [2, 20]", -2: "unsupported dtype combination for computeType",
-        -3: "unsupported transpose op", -4: "size limit (k beyond 2^17 or leading dimension too small)",
+        -3: "unsupported transpose op", -4: "size limit (padded k beyond 2^22 fast / 2^19 accurate, or leading dimension too small)",
         -5: "mode not implemented in this build", -6: "HIP launch failure"}
 
 

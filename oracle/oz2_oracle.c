@@ -487,8 +487,29 @@ static uint8_t conv8(int32_t x, unsigned j) {
     return (uint8_t)x;
 }
 
-/* residues R[j*(mr*n) + c*mr + r] = (A8[j] row r . B8[j] col c) mod p_j */
+/* residues R[j*(mr*n) + c*mr + r] = (A8[j] row r . B8[j] col c) mod p_j.  Up to kr = 2^17 the
+ * int32 product of the reference plus conv_32i_2_8u; beyond it the reference's int32 C32i wraps
+ * (every modulus but 256 then goes wrong) and this restatement takes the exact int64 residue, the
+ * value the build's k-chunked product computes (gemm_i8.hip). */
 int oz2o_residues(size_t mr, size_t n, size_t kr, unsigned N, const int8_t *A8, const int8_t *B8, uint8_t *R) {
+    if (kr > ((size_t)1 << 17)) {
+        for (unsigned j = 0; j < N; ++j) {
+            const int8_t *a = A8 + (size_t)j * mr * kr;
+            const int8_t *b = B8 + (size_t)j * n * kr;
+            uint8_t *o = R + (size_t)j * mr * n;
+            const int64_t p = oz2_p[j];
+#pragma omp parallel for schedule(static)
+            for (size_t c = 0; c < n; ++c) {
+                for (size_t r = 0; r < mr; ++r) {
+                    int64_t acc = 0;
+                    const int8_t *ar = a + r * kr, *bc = b + c * kr;
+                    for (size_t e = 0; e < kr; ++e) acc += (int64_t)ar[e] * (int64_t)bc[e];
+                    o[c * mr + r] = (uint8_t)(((acc % p) + p) % p);
+                }
+            }
+        }
+        return 0;
+    }
     for (unsigned j = 0; j < N; ++j) {
         const int8_t *a = A8 + (size_t)j * mr * kr;
         const int8_t *b = B8 + (size_t)j * n * kr;

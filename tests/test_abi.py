@@ -63,7 +63,8 @@ def test_work_size_and_errors_host_only():
     assert lib.gemmul8_gemm(*args(14, ta=2)) == -2          # complex A with real B
     assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2)) == -2  # complex types need COMPLEX_BIG_MATRIX_ENCODE
     assert lib.gemmul8_gemm(*args(14, ta=2, tb=2, tc=2, ct=1, opa=3, fast=0)) == -3  # op out of range
-    assert lib.gemmul8_gemm(*args(14, k=(1 << 17) + 1)) == -4
+    assert lib.gemmul8_gemm(*args(14, k=(1 << 22) + 1)) == -4          # fast: beyond the encode grid
+    assert lib.gemmul8_gemm(*args(14, k=(1 << 19) - 63, fast=0)) == -4  # accurate: int32 bound product
 
 
 def test_interposer_exports_and_has_no_runtime_dependency():

@@ -287,6 +287,36 @@ def test_long_k_signed_residue_path(fast):
                fast=fast)
 
 
+def test_k_beyond_int32_range_chunked():
+    """padded k > 2^17, where the reference's int32 products wrap: the residue product runs in
+    k-chunks of 2^16 whose residues add mod p (gemm_i8.hip), equal to the exact int64 residues of
+    the oracle (oz2o_residues); real and complex, fast mode"""
+    rng = np.random.default_rng(77)
+    check_full(randmat_np(rng, 9, 140000), randmat_np(rng, 140000, 7), 14)
+    check_full(randmat_np(rng, 5, 70000, dtype=np.complex128), randmat_np(rng, 70000, 6, dtype=np.complex128), 12)
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_k_chunks_forced(fast):
+    """the chunked product forced at small k (GEMMUL8_KCHUNK: chunks of 2 k-steps in a child
+    process) gives the same bits as one pass"""
+    import os
+    import subprocess
+    import sys
+    code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
+            "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
+            "rng = np.random.default_rng(5)\n"
+            f"check_full(randmat_np(rng, 300, 700), randmat_np(rng, 700, 260), 14, fast={fast})\n"
+            f"check_full(randmat_np(rng, 70, 333, dtype=np.complex128), randmat_np(rng, 333, 90, dtype=np.complex128), 9, fast={fast})\n"
+            "print('OK')")
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    env = dict(os.environ, GEMMUL8_KCHUNK="2")
+    r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
+
+
 @pytest.mark.parametrize("fast", [True, False])
 def test_padded_leading_dimensions(fast):
     """lda > m, ldb > k, ldc > m (odd, so C columns are not 16-byte aligned): same bits as the
