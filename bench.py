@@ -200,6 +200,13 @@ def main():
                     "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4), "traffic": traffic_from_profile(),
                     "kernel": "gemm_i8_kernel<RESIDUE> (int8 ops counted as FLOP, 2*m*n*k*num_moduli per launch)",
                     "avg_launch_ms": round(gemm_ms, 4)}
+        # measured live after the timed region: the same MFMA alone on uniformly random operand bytes
+        # (the residue distribution) in registers -- the clock the chip holds under that load bounds
+        # any int8 GEMM on such data
+        ceiling = G.mfma_ceiling()
+        if ceiling > 0:
+            roofline["data_bound_ceiling"] = round(ceiling, 1)
+            roofline["frac_of_data_bound_ceiling"] = round(achieved / ceiling, 4)
         extra = {"phase_ms": {"scaling": round(avg[0], 4), "int8_products": round(avg[1], 4),
                               "inverse_scaling": round(avg[3], 4)}}
         if not args.no_accuracy and A is not None:

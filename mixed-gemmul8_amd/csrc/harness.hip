@@ -129,9 +129,72 @@ __global__ void relerr_kernel(size_t count, const double *C, const double *C1, c
     err[i] = fabs(q1);
 }
 
+// The product kernel's data-bound ceiling: v_mfma_i32_32x32x32_i8 alone, 8 A and 8 B fragments of
+// uniformly random bytes (the residue distribution) held in registers and cycled through so the
+// operands change every instruction, two waves per SIMD, no memory traffic in the loop
+// (tools/probes/mfma_power.hip).  The clock the chip holds on it bounds what any int8 GEMM on
+// such operands can reach.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(256) void mfma_ceiling_kernel(int iters, int *out) {
+    unsigned x = threadIdx.x * 2654435761u + blockIdx.x * 40503u + 12345u;
+    v4i A[8], B[8];
+#pragma unroll
+    for (int f = 0; f < 8; ++f)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            x = x * 1664525u + 1013904223u;
+            A[f][q] = (int)x;
+            x = x * 1664525u + 1013904223u;
+            B[f][q] = (int)x;
+        }
+    v16i c0 = {}, c1 = {}, c2 = {}, c3 = {};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[0], B[j], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[1], B[(j + 1) & 7], c1, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[2], B[(j + 2) & 7], c2, 0, 0, 0);
+            c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[3], B[(j + 3) & 7], c3, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[4], B[(j + 4) & 7], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[5], B[(j + 5) & 7], c1, 0, 0, 0);
+            c2 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[6], B[(j + 6) & 7], c2, 0, 0, 0);
+            c3 = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[7], B[(j + 7) & 7], c3, 0, 0, 0);
+        }
+    }
+    out[blockIdx.x * 256 + threadIdx.x] = c0[0] + c1[1] + c2[2] + c3[3];
+}
+
 }  // namespace oz2h
 
 extern "C" {
+
+// int8 ops per second (TOPS) of mfma_ceiling_kernel over the whole chip; < 0 on failure
+double gemmul8_mfma_ceiling(void *stream, int iters) {
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess)
+        return -1.0;
+    const int blocks = 2 * cus;  // 8 waves per CU = 2 per SIMD
+    int *out = nullptr;
+    if (hipMalloc(&out, (size_t)blocks * 256 * sizeof(int)) != hipSuccess) return -1.0;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    oz2h::mfma_ceiling_kernel<<<blocks, 256, 0, st>>>(iters / 4 + 1, out);  // warm-up
+    (void)hipEventRecord(e0, st);
+    oz2h::mfma_ceiling_kernel<<<blocks, 256, 0, st>>>(iters, out);
+    (void)hipEventRecord(e1, st);
+    float ms = 0.f;
+    const bool ok = hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess && ms > 0.f;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(out);
+    if (!ok) return -1.0;
+    const double ops = 2.0 * 32 * 32 * 32 * 64.0 * iters * (double)blocks * 4;
+    return ops / (ms * 1e-3) / 1e12;
+}
 
 int gemmul8_randmat(void *stream, int dtype, size_t m, size_t n, void *A, double phi, unsigned long long seed) {
     hipStream_t st = static_cast<hipStream_t>(stream);

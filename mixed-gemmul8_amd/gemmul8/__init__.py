@@ -55,6 +55,8 @@ def _load():
     lib.gemmul8_randmat.argtypes = [p, i, sz, sz, p, ctypes.c_double, ctypes.c_ulonglong]
     lib.gemmul8_dd_gemm.argtypes = [p, sz, sz, sz, p, p, p, p]
     lib.gemmul8_relerr_dd.argtypes = [p, sz, p, p, p, p]
+    lib.gemmul8_mfma_ceiling.restype = ctypes.c_double
+    lib.gemmul8_mfma_ceiling.argtypes = [p, i]
     return lib
 
 
@@ -234,3 +236,9 @@ def relerr_dd(C, C1, C2, stream=None):
     cnt = s.numel()
     med = s[cnt // 2] if cnt & 1 else (s[cnt // 2] + s[cnt // 2 - 1]) * 0.5
     return float(s[-1]), float(med)
+
+
+def mfma_ceiling(iters=4000, stream=None):
+    """TOPS of v_mfma_i32_32x32x32_i8 alone on uniformly random operand bytes (the data-bound ceiling
+    of the int8 products on this GPU at the clock it holds under that load); synchronises."""
+    return float(lib.gemmul8_mfma_ceiling(_stream(stream), iters))
