@@ -30,10 +30,10 @@ enum : int { ENC_CONJ = 1, ENC_BTAIL = 2, ENC_KFIRST = 4 };
 // the result is THE symmetric residue of x (for p = 256 the two ties +-128 are the same byte).
 // Here x is reduced once modulo the product P of a group in f64, and each p of the group then
 // finishes in f32 from that value:
-//   pairs (N <= 17): P < 2^16, |x| < 2^72 (fast: log2M_fast[N] <= 66; accurate: 6 + log2M_accu <= 72),
-//     so rint(x/P) errs by < 2^20 and |t| < 2^22: ONE f32 step is exact (rint(t*fl(1/p)) is off
-//     from t/p by < 2^-23 |t/p|, less than the 1/(2p) separating t/p from a half-integer when p is
-//     odd; p = 256: exact product, a tie gives +-128, one byte);
+//   pairs (N <= 17): P < 2^16, |x| < 2^72 (fast: log2M_fast[N] < 65; accurate: 6 + log2M_accu[N] < 72),
+//     so the f64 step leaves |t| <= P/2 + |x| 2^-52 < 2^21, exact in f32, and ONE f32 step is exact
+//     (rint(t*fl(1/p)) is off from t/p by < 2^-23 |t/p| < 2^-9, less than the 1/(2p) separating t/p
+//     from a half-integer when p is odd; p = 256: exact product, a tie gives +-128, one byte);
 //   triples (N >= 18): P < 2^24, two f32 steps (the reference's own two).
 // Same residues as mod_8i either way (tools/probes/modcheck.py checks both forms against exact
 // integers over the magnitude range); per element, 7 f64 steps and 14 packed f32 steps at N = 14.
