@@ -37,7 +37,10 @@ constexpr int NTHREADS = 512;
 constexpr int STAGES = OZ2_STAGES;  // ring slots; DMA runs STAGES-1 k-steps ahead
 constexpr int SLOT = 2 * PANEL;     // A panel + B panel
 constexpr int LDS_BYTES = STAGES * SLOT;  // the epilogue reuses 64 KiB of it
-constexpr int GLDS_PER_STEP = 4;          // 1 KiB LDS-DMA pieces per wave per k-step (2 A + 2 B)
+constexpr int GLDS_PER_STEP = 4;
+// internal epilogue: RESIDUE whose residues are added mod p into the planes (k-chunks after the
+// first); a separate instantiation so the one-pass kernel's code stays as it is
+constexpr int EPI_RESIDUE_ADD = 3;          // 1 KiB LDS-DMA pieces per wave per k-step (2 A + 2 B)
 
 struct GemmArgs {
     const int8_t *A;
@@ -45,7 +48,6 @@ struct GemmArgs {
     size_t planeA, planeB;
     unsigned ksteps, mtiles, ntiles;
     unsigned kstride, k0;            // panels per tile in the planes, first k-step of this launch
-    int accumulate;                  // RESIDUE: add this launch's residues into the planes mod p
     void *out;
     size_t planeOut, ldo;
     int32_t *rowmax, *colmax;
@@ -200,7 +202,7 @@ template <int EPI>
 __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], int8_t *smem, int tid, int lane, int wr,
                                          int wc, unsigned tm, unsigned tn, unsigned j, bool active) {
     // accumulator map (32x32 fragments): col = lane & 31, row = (r & 3) + 8*(r >> 2) + 4*(lane >> 5)
-    if constexpr (EPI == (int)Epi::RESIDUE) {
+    if constexpr (EPI == (int)Epi::RESIDUE || EPI == EPI_RESIDUE_ADD) {
         const int p = g.p[j];
         uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
         // residues of the 4 x 2 fragments -> LDS, one fragment at a time (bounded VGPR use)
@@ -245,7 +247,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], i
             const int pm = x & 3;
             uint4 *dst = reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd);
             uint4 res = make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
-            if (g.accumulate) {  // k-chunked product: (earlier chunks + this chunk) mod p, bytewise
+            if constexpr (EPI == EPI_RESIDUE_ADD) {  // k-chunked product: (earlier chunks + this chunk) mod p
                 const uint4 prev = *dst;
                 res = make_uint4(add_mod_bytes(res.x, prev.x, (uint32_t)p), add_mod_bytes(res.y, prev.y, (uint32_t)p),
                                  add_mod_bytes(res.z, prev.z, (uint32_t)p), add_mod_bytes(res.w, prev.w, (uint32_t)p));
@@ -350,7 +352,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     };
 
     v16i acc[4][2];
-    const int acc0 = (EPI == (int)Epi::RESIDUE && g.biased) ? g.bias[j] : 0;
+    const int acc0 = ((EPI == (int)Epi::RESIDUE || EPI == EPI_RESIDUE_ADD) && g.biased) ? g.bias[j] : 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -490,7 +492,6 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     }
     g.kstride = g.ksteps;
     g.k0 = 0;
-    g.accumulate = 0;
     dim3 grid((unsigned)(L.mtiles * L.ntiles), nplanes);
     // GEMMUL8_FORCE_FLAT_DMA=1 takes the 64-bit path at any size (tests cover it with small shapes)
     const char *ff = getenv("GEMMUL8_FORCE_FLAT_DMA");
@@ -509,8 +510,8 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         for (unsigned k0 = 0; k0 < g.kstride; k0 += chunk) {
             g.k0 = k0;
             g.ksteps = g.kstride - k0 < chunk ? g.kstride - k0 : chunk;
-            g.accumulate = k0 > 0;
-            buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0);
+            if (k0 == 0) buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0);
+            else buf ? OZ2_GEMM(EPI_RESIDUE_ADD, 1) : OZ2_GEMM(EPI_RESIDUE_ADD, 0);
         }
         return;
     }
