@@ -12,6 +12,8 @@
 // template parameter (19 instantiations) so every plane load is unguarded and
 // the accumulation fully unrolled; the weights arrive as kernel arguments (the
 // reference uploads them to __constant__ on every call, gemmul8.cu:236-241).
+#include <utility>
+
 #include "oz2_split.hpp"
 
 namespace oz2 {
@@ -51,12 +53,49 @@ __device__ __forceinline__ double crt_value(const CrtParams &cp, const uint8_t (
     }
 }
 
+// The same value with the weights and M as compile-time constants of (N, NUMM1) (the table of
+// make_crt_params): passed as kernel arguments, the 2N weights overflow the SGPRs and the compiler
+// parks them in VGPR lanes (~35 v_readlane per element); as literals they are rematerialised where
+// used.  i = 0..N-1 in order for each of C1 and C2, as in crt_value.
+template <unsigned N, bool NUMM1, unsigned I> __device__ __forceinline__ constexpr double w_hi() {
+    if constexpr (NUMM1) return oz2_NMi_1[N - 2][I];
+    else if constexpr (N >= 8) return oz2_NMi_2[N - 8][I][0];
+    else return 0.0;
+}
+template <unsigned N, unsigned I> __device__ __forceinline__ constexpr double w_lo() {
+    if constexpr (N >= 8) return oz2_NMi_2[N - 8][I][1];
+    else return 0.0;
+}
+template <unsigned N, bool NUMM1, unsigned... I>
+__device__ __forceinline__ double crt_value_const(const uint8_t (&r)[N], std::integer_sequence<unsigned, I...>) {
+    constexpr double invM = oz2_invM[N - 2], M1 = oz2_M_hi[N - 2], M2 = oz2_M_lo[N - 2];
+    if constexpr (NUMM1) {
+        double C = 0.0;
+        ((C = __builtin_fma(w_hi<N, true, I>(), (double)r[I], C)), ...);
+        const double quot = -__builtin_rint(C * invM);
+        return __builtin_fma(quot, M1, C);
+    } else {
+        double C1 = 0.0, C2 = 0.0;
+        ((C1 = __builtin_fma(w_hi<N, false, I>(), (double)r[I], C1)), ...);
+        ((C2 = __builtin_fma(w_lo<N, I>(), (double)r[I], C2)), ...);
+        const double quot = -__builtin_rint(__builtin_fma(C1, invM, C2 * invM));
+        const double t1 = __builtin_fma(quot, M1, C1) + C2;
+        return __builtin_fma(quot, M2, t1);
+    }
+}
+
 // residues of rows [off, off+8) of every plane; the fast path is one 8-byte load per plane
 template <unsigned N>
 __device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fast, int nr, uint64_t (&w)[N]) {
     if (fast) {
+        // one per-lane pointer stepped plane by plane (N scalar plane bases would spill the SGPRs)
+        const uint8_t *q = a.R + off;
 #pragma unroll
-        for (unsigned i = 0; i < N; ++i) w[i] = *reinterpret_cast<const uint64_t *>(a.R + i * a.planeR + off);
+        for (unsigned i = 0; i < N; ++i) {
+            w[i] = *reinterpret_cast<const uint64_t *>(q);
+            q += a.planeR;
+            asm volatile("" : "+v"(q));
+        }
     } else {
 #pragma unroll
         for (unsigned i = 0; i < N; ++i) {
@@ -160,7 +199,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
 #pragma unroll
                 for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
                 const int sft = (int)sa[e] + sB;
-                const double vr = scalbn(crt_value<N, NUMM1>(a.cp, r), sft);
+                const double vr = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}), sft);
                 if constexpr (OT == 0) {
                     wb[lane * CRT_ROWS + e] = vr;
                 } else if constexpr (OT == 1) {
@@ -168,7 +207,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
                 } else {
 #pragma unroll
                     for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(wi[i] >> (8 * e));
-                    const double vi = scalbn(crt_value<N, NUMM1>(a.cp, r), sft);
+                    const double vi = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}), sft);
                     if constexpr (OT == 2) wb[lane * CRT_ROWS + e] = make_double2(vr, vi);
                     else wb[lane * CRT_ROWS + e] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
                 }
