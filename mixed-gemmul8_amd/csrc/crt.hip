@@ -10,8 +10,9 @@
 // reads one 8-byte word from each of the N residue planes (coalesced across the
 // wave: 512 B per plane per wave instruction) and writes 8 outputs.  N is a
 // template parameter (19 instantiations) so every plane load is unguarded and
-// the accumulation fully unrolled; the weights arrive as kernel arguments (the
-// reference uploads them to __constant__ on every call, gemmul8.cu:236-241).
+// the accumulation fully unrolled; the weights are compile-time constants of the
+// instantiation (the reference uploads them to __constant__ on every call,
+// gemmul8.cu:236-241).
 #include <utility>
 
 #include "oz2_split.hpp"
@@ -29,34 +30,12 @@ struct CrtArgs {
     void *C;
     size_t ldc;
     double ar, ai, br, bi;
-    CrtParams cp;
 };
 
-template <unsigned N, bool NUMM1>
-__device__ __forceinline__ double crt_value(const CrtParams &cp, const uint8_t (&r)[N]) {
-    if (NUMM1) {
-        double C = 0.0;
-#pragma unroll
-        for (unsigned i = 0; i < N; ++i) C = __builtin_fma(cp.w_hi[i], (double)r[i], C);
-        const double quot = -__builtin_rint(C * cp.invM);
-        return __builtin_fma(quot, cp.M1, C);
-    } else {
-        double C1 = 0.0, C2 = 0.0;
-#pragma unroll
-        for (unsigned i = 0; i < N; ++i) {
-            C1 = __builtin_fma(cp.w_hi[i], (double)r[i], C1);
-            C2 = __builtin_fma(cp.w_lo[i], (double)r[i], C2);
-        }
-        const double quot = -__builtin_rint(__builtin_fma(C1, cp.invM, C2 * cp.invM));
-        const double t1 = __builtin_fma(quot, cp.M1, C1) + C2;
-        return __builtin_fma(quot, cp.M2, t1);
-    }
-}
-
-// The same value with the weights and M as compile-time constants of (N, NUMM1) (the table of
-// make_crt_params): passed as kernel arguments, the 2N weights overflow the SGPRs and the compiler
-// parks them in VGPR lanes (~35 v_readlane per element); as literals they are rematerialised where
-// used.  i = 0..N-1 in order for each of C1 and C2, as in crt_value.
+// CRT value of one element (inverse_scaling.hpp:35-62 numM = 1, :138-172 numM = 2) with the weights
+// and M as compile-time constants of (N, NUMM1), the table make_crt_params reads: passed as kernel
+// arguments the 2N weights overflowed the SGPRs and were parked in VGPR lanes.  Each of C1 and C2
+// accumulates i = 0..N-1 in order, as the reference does.
 template <unsigned N, bool NUMM1, unsigned I> __device__ __forceinline__ constexpr double w_hi() {
     if constexpr (NUMM1) return oz2_NMi_1[N - 2][I];
     else if constexpr (N >= 8) return oz2_NMi_2[N - 8][I][0];
@@ -290,7 +269,6 @@ void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const i
         a.br = ((const float *)beta)[0]; a.bi = ((const float *)beta)[1];
         break;
     }
-    a.cp = CP;
     const unsigned gx = (unsigned)((L.m + 256 * CRT_ROWS - 1) / (256 * CRT_ROWS));
     const unsigned gy = (unsigned)(L.n < 65535 ? L.n : 65535);
     dim3 grid(gx, gy);

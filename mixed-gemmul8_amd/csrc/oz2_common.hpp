@@ -91,13 +91,11 @@ __host__ __device__ inline size_t panel_offset(size_t v, size_t kk, size_t kstep
 }
 
 // ------------------------------------------------------------------
-// CRT constants passed by value (kernarg), replacing the reference's
-// per-call hipMemcpyToSymbol into __constant__ (gemmul8.cu:236-241)
+// CRT variant of a call: num_moduli and whether the single-double form (numM = 1) applies.  The
+// weights, M and 1/M are compile-time constants of that pair in crt.hip (from oz2_tables.inc); the
+// reference uploads them to __constant__ on every call (gemmul8.cu:236-241).
 // ------------------------------------------------------------------
 struct CrtParams {
-    double w_hi[OZ2_MAX_MODULI];  // NMi_2 hi (numM = 2) or NMi_1 (numM = 1)
-    double w_lo[OZ2_MAX_MODULI];  // NMi_2 lo
-    double invM, M1, M2;
     int numM1;
     unsigned N;
 };
@@ -124,20 +122,8 @@ static inline ModParams make_mod_params(unsigned N) {
 
 static inline CrtParams make_crt_params(unsigned N, bool force_numM1) {
     CrtParams C{};
-    const unsigned t = N - 2;
-    C.numM1 = (oz2_numM[t] == 1) || force_numM1;
+    C.numM1 = (oz2_numM[N - 2] == 1) || force_numM1;  // float outputs: the no-numM overload (inverse_scaling.hpp:823-856)
     C.N = N;
-    for (unsigned i = 0; i < N; ++i) {
-        if (C.numM1) {
-            C.w_hi[i] = oz2_NMi_1[t][i];
-        } else {
-            C.w_hi[i] = oz2_NMi_2[N - 8][i][0];
-            C.w_lo[i] = oz2_NMi_2[N - 8][i][1];
-        }
-    }
-    C.invM = oz2_invM[t];
-    C.M1 = oz2_M_hi[t];
-    C.M2 = oz2_M_lo[t];
     return C;
 }
 
