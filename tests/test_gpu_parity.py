@@ -396,3 +396,37 @@ def test_offset_pointers(fast):
     torch.cuda.synchronize()
     Cg = dC.cpu().numpy().reshape((m, n), order="F")
     assert np.asfortranarray(Cg).tobytes() == np.asfortranarray(C_ref).tobytes()
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_integer_inputs_at_scale(fast):
+    """Size-independent property at a size the oracle cannot check quickly: for integer inputs the
+    exact product is known (float64 matmul of integers below 2^53 is exact), and the emulation
+    must stay within the Ozaki-II bound |C - AB| <= 2^-44 (|A| |B|) elementwise (its error is the
+    CRT's double-double rounding only: measured 6e-12 relative on the oracle-checked small case,
+    tools/probes/intcheck.py).  16384 x 12288 x 1536 real, 4096 x 3072 x 1024 complex."""
+    torch = _torch()
+    import gemmul8 as G
+    g = torch.Generator(device="cuda").manual_seed(1234 + fast)
+
+    def check(C, exact, bound):
+        err = (C - exact).abs()
+        assert bool((err <= bound * 2.0 ** -44).all()), float((err / bound).max())
+
+    m, n, k = 16384, 12288, 1536
+    A = torch.randint(-1000, 1001, (k, m), generator=g, device="cuda").to(torch.float64)  # column-major m x k
+    B = torch.randint(-1000, 1001, (n, k), generator=g, device="cuda").to(torch.float64)  # column-major k x n
+    C = torch.empty((n, m), dtype=torch.float64, device="cuda")
+    W = G.alloc_work(m, n, k, 14)
+    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C, m, 14, fast, W)
+    check(C, B @ A, B.abs() @ A.abs())  # (n x k)(k x m): the column-major A B
+    del W, C
+    mc, nc, kc = 4096, 3072, 1024
+    Ac = torch.complex(torch.randint(-500, 501, (kc, mc), generator=g, device="cuda").double(),
+                       torch.randint(-500, 501, (kc, mc), generator=g, device="cuda").double())
+    Bc = torch.complex(torch.randint(-500, 501, (nc, kc), generator=g, device="cuda").double(),
+                       torch.randint(-500, 501, (nc, kc), generator=g, device="cuda").double())
+    Cc = torch.empty((nc, mc), dtype=torch.complex128, device="cuda")
+    Wc = G.alloc_work(mc, nc, kc, 12, G.COMPLEX_BIG_MATRIX_ENCODE)
+    G.gemm(0, 0, mc, nc, kc, 1.0, Ac, mc, Bc, kc, 0.0, Cc, mc, 12, fast, Wc, G.COMPLEX_BIG_MATRIX_ENCODE)
+    check(Cc, Bc @ Ac, 2.0 * (Bc.abs() @ Ac.abs()))
