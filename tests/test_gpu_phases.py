@@ -45,6 +45,9 @@ def _same(a, b):
     (300, 260, 500, 14, True, "f64"),
     (257, 190, 333, 9, False, "f64"),
     (200, 128, 256, 6, True, "f32"),
+    # (m + n) k >= 2^25: the phase entry points fork operand B's split onto the second stream
+    (2048, 1900, 8400, 14, True, "f64"),
+    (1900, 2048, 8400, 11, False, "f64"),
 ])
 def test_moduli_ranges_compose(m, n, k, N, fast, dt):
     import torch
