@@ -14,7 +14,8 @@ the single-GPU ``gemmul8.gemm`` on the same inputs.
                    ranks combine those column maxima (n int32) with one MAX all-reduce before
                    encoding.  This is the partition bench.py scales.
 ``matmul_moduli``  rank r owns the moduli [j0, j1): it computes the shifts (cheap, HBM-bound),
-                   the slices and the residue planes of its moduli only, and sends its planes
+                   the slices and the residue planes of its moduli only, sending each plane as
+                   soon as its product is launched (the send overlaps the next plane's product),
                    to the root, which receives every rank's planes concurrently (each sender on
                    its own xGMI link) into its workspace and runs the CRT over all N planes.
                    Bytes moved: (N - N_root) * m * n, one byte per residue.  The alternative of
@@ -90,8 +91,8 @@ class HipOps:
         recombine(m, n, k, N, 1.0, 0.0, Ct, m, work)
         return Ct.t()
 
-    def partial(self, A, B, num_moduli, fastmode, out_dtype, j0, j1, need_shifts):
-        """Residue planes [j0, j1) -> (uint8 [j1 - j0, plane] view, state for the root)."""
+    def begin(self, A, B, num_moduli, fastmode, out_dtype, j0, j1, need_shifts):
+        """Shifts + slices of moduli [j0, j1) (no products yet) -> state for product() / finish()."""
         if A.is_complex():
             raise NotImplementedError("modulus sharding covers real operands")
         m, k = A.shape
@@ -100,10 +101,14 @@ class HipOps:
         st = {"m": m, "n": n, "k": k, "N": num_moduli, "work": work, "dtype": out_dtype, "device": A.device}
         if j1 > j0:
             split(OP_T, OP_T, m, n, k, A, k, B, n, num_moduli, fastmode, work, out_dtype, j0, j1)
-            products(m, n, k, num_moduli, work, j0, j1)
         elif need_shifts:  # a root that owns no modulus still needs the shifts (one unused slice plane)
             split(OP_T, OP_T, m, n, k, A, k, B, n, num_moduli, fastmode, work, out_dtype, 0, 1)
-        return residue_planes(work, m, n, k, num_moduli, j0, j1), st
+        return st
+
+    def product(self, st, j):
+        """Residue plane j (one launch on the current stream) -> its uint8 [plane] view."""
+        products(st["m"], st["n"], st["k"], st["N"], st["work"], j, j + 1)
+        return residue_planes(st["work"], st["m"], st["n"], st["k"], st["N"], j, j + 1)[0]
 
     def all_planes(self, st):
         return residue_planes(st["work"], st["m"], st["n"], st["k"], st["N"])
@@ -167,27 +172,40 @@ def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=
 def matmul_moduli(A, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, root=0, ops=None):
     """C = A @ B with the moduli sharded over the ranks of `group` (A, B replicated).
 
-    Returns C on the root, None on the other ranks."""
+    Each rank computes its planes one modulus at a time and sends each as soon as it is launched:
+    with RCCL the send of plane j runs on the communication stream behind the products of plane j
+    while the products of plane j + 1 run, and the root receives every rank's planes concurrently
+    (one xGMI link per sender) while computing its own.  Returns C on the root, None elsewhere."""
     ops = ops or HipOps()
     out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
     rank, world = _group_info(group)
     parts = moduli_partition(num_moduli, world)
     j0, j1 = parts[rank]
-    planes, st = ops.partial(A, B, num_moduli, fastmode, out_dtype, j0, j1, rank == root)
-    ops.sync()
+    # the gloo backend reads device tensors without waiting on the compute stream
+    host_sync = dist.get_backend(group) != "nccl"
+    st = ops.begin(A, B, num_moduli, fastmode, out_dtype, j0, j1, rank == root)
     groot = dist.get_global_rank(group, root) if group is not None else root
     if rank != root:
-        if j1 > j0:
-            dist.send(planes, dst=groot, group=group)
+        reqs = []
+        for j in range(j0, j1):
+            plane = ops.product(st, j)
+            if host_sync:
+                ops.sync()
+            reqs.append(dist.isend(plane, dst=groot, group=group))
+        for q in reqs:
+            q.wait()
         return None
     allp = ops.all_planes(st)
     reqs = []
     for r in range(world):
         a, b = parts[r]
-        if r == root or b == a:
+        if r == root:
             continue
         src = dist.get_global_rank(group, r) if group is not None else r
-        reqs.append(dist.irecv(allp[a:b], src=src, group=group))
+        for j in range(a, b):  # one receive per plane, in the sender's order
+            reqs.append(dist.irecv(allp[j], src=src, group=group))
+    for j in range(j0, j1):
+        ops.product(st, j)
     for q in reqs:
         q.wait()
     return ops.finish(st)

@@ -50,14 +50,16 @@ class OracleOps:
         C = self.O.crt(self.O.residues(A8, B8), sA, sB, npt)
         return torch.from_numpy(np.ascontiguousarray(C))
 
-    def partial(self, A, B, N, fast, out_dtype, j0, j1, need_shifts):
+    def begin(self, A, B, N, fast, out_dtype, j0, j1, need_shifts):
         A8, B8, sA, sB = self.O.scaling(A.numpy(), B.numpy(), N, fast)
         full = self.O.residues(A8, B8)
-        R = np.zeros_like(full)  # only this rank's planes; the root must receive the rest
-        R[j0:j1] = full[j0:j1]
-        Rt = torch.from_numpy(R).reshape(N, -1)
+        Rt = torch.zeros((N, full[0].size), dtype=torch.uint8)  # planes arrive one by one
         npt = torch.empty((), dtype=out_dtype).numpy().dtype
-        return Rt[j0:j1], {"R": Rt, "shape": full.shape, "sA": sA, "sB": sB, "dtype": npt}
+        return {"R": Rt, "full": full, "shape": full.shape, "sA": sA, "sB": sB, "dtype": npt}
+
+    def product(self, st, j):
+        st["R"][j] = torch.from_numpy(st["full"][j].reshape(-1))
+        return st["R"][j]
 
     def all_planes(self, st):
         return st["R"]

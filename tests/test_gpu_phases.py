@@ -130,12 +130,14 @@ def test_moduli_shards_assembled_on_root():
     ref = _single(A, B, N, True, torch.float64)
     ops = GD.HipOps()
     parts = GD.moduli_partition(N, 4)
-    shards = [ops.partial(A, B, N, True, torch.float64, a, b, r == 0) for r, (a, b) in enumerate(parts)]
-    root_st = shards[0][1]
+    states = [ops.begin(A, B, N, True, torch.float64, a, b, r == 0) for r, (a, b) in enumerate(parts)]
+    root_st = states[0]
     allp = ops.all_planes(root_st)
     for r, (a, b) in enumerate(parts):
-        if r:
-            allp[a:b].copy_(shards[r][0])
+        for j in range(a, b):  # plane by plane, as matmul_moduli sends them
+            plane = ops.product(states[r], j)
+            if r:
+                allp[j].copy_(plane)
     out = ops.finish(root_st)
     torch.cuda.synchronize()
     assert _same(out, ref)
@@ -173,3 +175,51 @@ def test_low_memory_mode_complex():
         out.append(Ct)
     torch.cuda.synchronize()
     assert _same(out[0], out[1])
+
+
+_MULTI_RANK_CHILD = r'''
+import os, sys
+import torch
+import torch.distributed as dist
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+from gemmul8 import dist as GD
+from test_gpu_phases import _rand, _single, _same
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(0)  # the ranks share the one GPU; gloo carries the messages
+dist.init_process_group("gloo")
+try:
+    m, n, k, N = 700, 300, 400, 14
+    A, B = _rand(m, k, 11, torch.float64), _rand(k, n, 12, torch.float64)
+    ok = True
+    for fast in (True, False):
+        ref = _single(A, B, N, fast, torch.float64) if rank == 0 else None
+        C = GD.matmul_moduli(A, B, N, fast)
+        if rank == 0:
+            ok &= _same(C, ref)
+        r0, r1 = GD.row_partition(m, world)[rank]
+        Cr = GD.matmul_rows(A[r0:r1].contiguous(), B, N, fast, gather=True)
+        if rank == 0:
+            ok &= _same(Cr, ref)
+    dist.barrier()
+    if rank == 0:
+        print("RESULT", "OK" if ok else "MISMATCH")
+finally:
+    dist.destroy_process_group()
+'''
+
+
+def test_dist_three_ranks_on_one_gpu_gloo():
+    """gemmul8.dist with three processes on the one GPU (gloo messages): the modulus partition with
+    its per-plane sends and the row partition (accurate mode: the MAX all-reduce of the column
+    bounds) on the native kernels, bit-identical to the single call"""
+    import subprocess
+    import sys
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "--no-python", sys.executable, "-c",
+           _MULTI_RANK_CHILD, tdir, os.path.join(root, "mixed-gemmul8_amd")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "RESULT OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
