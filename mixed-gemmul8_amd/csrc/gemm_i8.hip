@@ -30,6 +30,20 @@ namespace oz2 {
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v16i __attribute__((ext_vector_type(16)));
 
+// MFMA shape of the products: 1 = v_mfma_i32_16x16x64_i8 (8 x 4 tiles of 16 x 16 per wave), 0 =
+// v_mfma_i32_32x32x32_i8 (4 x 2 tiles of 32 x 32).  Same operand bytes, LDS reads and accumulator
+// registers per k-step; the 16x16 form moves a quarter of the accumulator data per instruction.
+#ifndef OZ2_MFMA16
+#define OZ2_MFMA16 1
+#endif
+#if OZ2_MFMA16
+typedef v4i AccTile;
+constexpr int ACC_I = 8, ACC_J = 4;  // 16-row x 16-col tiles of a wave's 128 x 64
+#else
+typedef v16i AccTile;
+constexpr int ACC_I = 4, ACC_J = 2;  // 32 x 32 tiles
+#endif
+
 constexpr int NTHREADS = 512;
 #ifndef OZ2_STAGES
 #define OZ2_STAGES 4
@@ -149,6 +163,56 @@ __device__ __forceinline__ uint32_t add_mod_bytes(uint32_t a, uint32_t b, uint32
     return r;
 }
 
+#if OZ2_MFMA16
+// One k-step (64 deep) of fragments for a wave: 8 row blocks of 16 of A, 4 column blocks of 16 of B.
+// The panel layout [s:2][blk:8][h:2][r:32][16 B] (vector 32 blk + r, k 32 s + 16 h + byte) is read
+// with per-lane addresses: lane l = r16 + 16 q takes the 16 k-bytes 16q.. of vector r16 of the block,
+// i.e. (s, h) = (q >> 1, q & 1); A and B lanes pair the same k-bytes, which is all the dot product
+// needs.  Each group of 16 lanes reads 256 contiguous bytes (conflict-free).
+struct Frags {
+    v4i a[8];
+    v4i b[4];
+};
+__device__ __forceinline__ int frag_lane_offset(int lane) {
+    const int q = lane >> 4;
+    return (q >> 1) * 8192 + ((q & 1) * 32 + (lane & 15)) * 16;
+}
+__device__ __forceinline__ void read_frags(Frags &f, const int8_t *slot, int wr, int wc, int lane) {
+    const int8_t *base = slot + frag_lane_offset(lane);
+    if (OZ2_ABLATE == 3 || OZ2_ABLATE == 4) {  // probe: no LDS reads (operands = slot address bits)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f.a[i] = v4i{} + (int)(uintptr_t)slot + i;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) f.b[jj] = v4i{} + (int)(uintptr_t)slot + jj;
+        return;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)  // rows 16 i.. of the wave's 128: block wr*4 + i/2, half i&1
+        f.a[i] = *reinterpret_cast<const v4i *>(base + (wr * 4 + (i >> 1)) * 1024 + (i & 1) * 256);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)  // columns 16 jj.. of the wave's 64: block wc*2 + jj/2, half jj&1
+        f.b[jj] = *reinterpret_cast<const v4i *>(base + PANEL + (wc * 2 + (jj >> 1)) * 1024 + (jj & 1) * 256);
+}
+__device__ __forceinline__ void mfma_step(AccTile (&acc)[ACC_I][ACC_J], const Frags &f) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            if (OZ2_ABLATE == 2 || OZ2_ABLATE == 4) {
+                acc[i][jj][0] += f.a[i][0] ^ f.b[jj][1];
+            } else {
+                acc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[i], f.b[jj], acc[i][jj], 0, 0, 0);
+            }
+        }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+}
+// accumulator map (16x16 tiles): col = lane & 15, row = 4 (lane >> 4) + e, e = 0..3
+__device__ __forceinline__ int acc_row(int i, int e, int lane) { return i * 16 + 4 * (lane >> 4) + e; }
+__device__ __forceinline__ int acc_col(int jj, int lane) { return jj * 16 + (lane & 15); }
+constexpr int ACC_E = 4;
+#else
 // One k-step of fragments for a wave: 4 row blocks of A, 2 column blocks of B, both 32-deep halves.
 struct Frags {
     v4i a[2][4];
@@ -178,7 +242,7 @@ __device__ __forceinline__ void read_frags(Frags &f, const int8_t *slot, int wr,
     }
 }
 
-__device__ __forceinline__ void mfma_step(v16i (&acc)[4][2], const Frags &f) {
+__device__ __forceinline__ void mfma_step(AccTile (&acc)[ACC_I][ACC_J], const Frags &f) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
@@ -196,12 +260,17 @@ __device__ __forceinline__ void mfma_step(v16i (&acc)[4][2], const Frags &f) {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// accumulator map (32x32 tiles): col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+__device__ __forceinline__ int acc_row(int i, int e, int lane) { return i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5); }
+__device__ __forceinline__ int acc_col(int jj, int lane) { return jj * 32 + (lane & 31); }
+constexpr int ACC_E = 16;
+#endif
+
 // Epilogues over the 8 compute waves' accumulators (active = this wave holds a 128 x 64 block;
 // every thread of the block must call it: it contains block barriers).
 template <int EPI>
-__device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], int8_t *smem, int tid, int lane, int wr,
+__device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I][ACC_J], int8_t *smem, int tid, int lane, int wr,
                                          int wc, unsigned tm, unsigned tn, unsigned j, bool active) {
-    // accumulator map (32x32 fragments): col = lane & 31, row = (r & 3) + 8*(r >> 2) + 4*(lane >> 5)
     if constexpr (EPI == (int)Epi::RESIDUE || EPI == EPI_RESIDUE_ADD) {
         const int p = g.p[j];
         uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
@@ -209,16 +278,16 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], i
         auto park = [&](auto &&res) {
             if (!active) return;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
-                for (int jj = 0; jj < 2; ++jj) {
-                    const int col = wc * 64 + jj * 32 + (lane & 31);
+                for (int jj = 0; jj < ACC_J; ++jj) {
+                    const int col = wc * 64 + acc_col(jj, lane);
 #pragma unroll
-                    for (int gq = 0; gq < 4; ++gq) {
+                    for (int gq = 0; gq < ACC_E / 4; ++gq) {  // four consecutive rows per dword
                         uint32_t w = 0;
 #pragma unroll
                         for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][4 * gq + e]) << (8 * e);
-                        const int rdw = wr * 32 + i * 8 + 2 * gq + (lane >> 5);
+                        const int rdw = (wr * 128 + acc_row(i, 4 * gq, lane)) >> 2;
                         lo[col * 64 + (rdw ^ (col & 31))] = w;
                     }
                     __builtin_amdgcn_sched_barrier(0);
@@ -262,26 +331,30 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], i
             cmax[tid] = 0;
         }
         __syncthreads();
+        // rows: lanes sharing a row are those with the same row part of the lane index; columns: the same
+        // column part (32x32: lane & 31 / lane >> 5; 16x16: lane >> 4 / lane & 15)
+        constexpr int COLS_PER_TILE = OZ2_MFMA16 ? 16 : 32;
 #pragma unroll
-        for (int i = 0; i < 4 && active; ++i)
+        for (int i = 0; i < ACC_I && active; ++i)
 #pragma unroll
-            for (int rr = 0; rr < 16; ++rr) {
+            for (int rr = 0; rr < ACC_E; ++rr) {
                 int v = 0;
 #pragma unroll
-                for (int jj = 0; jj < 2; ++jj) v = max(v, abs(acc[i][jj][rr]));
+                for (int jj = 0; jj < ACC_J; ++jj) v = max(v, abs(acc[i][jj][rr]));
 #pragma unroll
-                for (int d = 16; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 32));
-                if ((lane & 31) == 0) atomicMax(&rmax[wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5)], v);
+                for (int d = COLS_PER_TILE / 2; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, COLS_PER_TILE));
+                if ((lane & (COLS_PER_TILE - 1)) == 0) atomicMax(&rmax[wr * 128 + acc_row(i, rr, lane)], v);
             }
 #pragma unroll
-        for (int jj = 0; jj < 2 && active; ++jj) {
+        for (int jj = 0; jj < ACC_J && active; ++jj) {
             int v = 0;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
-                for (int rr = 0; rr < 16; ++rr) v = max(v, abs(acc[i][jj][rr]));
-            v = max(v, __shfl_xor(v, 32));
-            if (lane < 32) atomicMax(&cmax[wc * 64 + jj * 32 + lane], v);
+                for (int rr = 0; rr < ACC_E; ++rr) v = max(v, abs(acc[i][jj][rr]));
+#pragma unroll
+            for (int d = COLS_PER_TILE; d < 64; d <<= 1) v = max(v, __shfl_xor(v, d));
+            if (lane < COLS_PER_TILE) atomicMax(&cmax[wc * 64 + acc_col(jj, lane)], v);
         }
         __syncthreads();
         if (tid < 256) {
@@ -291,13 +364,13 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, v16i (&acc)[4][2], i
     } else if (active) {  // RAW int32 (plane 0): validation path
         int32_t *out = static_cast<int32_t *>(g.out);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
-            for (int jj = 0; jj < 2; ++jj)
+            for (int jj = 0; jj < ACC_J; ++jj)
 #pragma unroll
-                for (int rr = 0; rr < 16; ++rr) {
-                    const size_t row = (size_t)tm * 256 + wr * 128 + i * 32 + (rr & 3) + 8 * (rr >> 2) + 4 * (lane >> 5);
-                    const size_t col = (size_t)tn * 256 + wc * 64 + jj * 32 + (lane & 31);
+                for (int rr = 0; rr < ACC_E; ++rr) {
+                    const size_t row = (size_t)tm * 256 + wr * 128 + acc_row(i, rr, lane);
+                    const size_t col = (size_t)tn * 256 + wc * 64 + acc_col(jj, lane);
                     out[col * g.ldo + row] = acc[i][jj][rr];
                 }
     }
@@ -351,12 +424,12 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
         }
     };
 
-    v16i acc[4][2];
+    AccTile acc[ACC_I][ACC_J];
     const int acc0 = ((EPI == (int)Epi::RESIDUE || EPI == EPI_RESIDUE_ADD) && g.biased) ? g.bias[j] : 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
-        for (int jj = 0; jj < 2; ++jj) acc[i][jj] = v16i{} + acc0;  // splat
+        for (int jj = 0; jj < ACC_J; ++jj) acc[i][jj] = AccTile{} + acc0;  // splat
 
     const unsigned K = g.ksteps;
     constexpr unsigned D = STAGES - 1;  // prefetch distance in k-steps
