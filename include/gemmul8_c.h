@@ -113,8 +113,9 @@ int gemmul8_dd_gemm(void *stream, size_t m, size_t n, size_t k, const double *A,
                     double *C2);
 /* err[i] = |C[i] - (C1[i] + C2[i])| / |C1[i] + C2[i]| evaluated in double-double (eval.hpp:317-338). */
 int gemmul8_relerr_dd(void *stream, size_t count, const double *C, const double *C1, const double *C2, double *err);
-/* Data-bound ceiling of the int8 products: TOPS of v_mfma_i32_32x32x32_i8 alone on uniformly random
- * operand bytes held in registers (2 waves per SIMD, `iters` x 64 MFMAs per wave); synchronises. */
+/* Data-bound ceiling of the int8 products: TOPS of the better of v_mfma_i32_32x32x32_i8 and
+ * v_mfma_i32_16x16x64_i8 alone on uniformly random operand bytes held in registers (2 waves per
+ * SIMD, the ops of `iters` x 64 32x32x32 MFMAs per wave); synchronises. */
 double gemmul8_mfma_ceiling(void *stream, int iters);
 
 #ifdef __cplusplus

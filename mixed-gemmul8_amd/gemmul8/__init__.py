@@ -239,6 +239,6 @@ def relerr_dd(C, C1, C2, stream=None):
 
 
 def mfma_ceiling(iters=4000, stream=None):
-    """TOPS of v_mfma_i32_32x32x32_i8 alone on uniformly random operand bytes (the data-bound ceiling
-    of the int8 products on this GPU at the clock it holds under that load); synchronises."""
+    """TOPS of the int8 MFMA alone (the better of 32x32x32 and 16x16x64) on uniformly random operand
+    bytes: the data-bound ceiling of the int8 products at the clock the GPU holds under that load."""
     return float(lib.gemmul8_mfma_ceiling(_stream(stream), iters))
