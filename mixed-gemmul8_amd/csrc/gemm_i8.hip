@@ -193,18 +193,20 @@ __device__ __forceinline__ void read_frags(Frags &f, const int8_t *slot, int wr,
     for (int jj = 0; jj < 4; ++jj)  // columns 16 jj.. of the wave's 64: block wc*2 + jj/2, half jj&1
         f.b[jj] = *reinterpret_cast<const v4i *>(base + PANEL + (wc * 2 + (jj >> 1)) * 1024 + (jj & 1) * 256);
 }
+#ifndef OZ2_MFMA_ORDER
+#define OZ2_MFMA_ORDER 0  // probe builds: 0 = A-major (4 consecutive MFMAs share an A fragment), 1 = B-major
+#endif
 __device__ __forceinline__ void mfma_step(AccTile (&acc)[ACC_I][ACC_J], const Frags &f) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-            if (OZ2_ABLATE == 2 || OZ2_ABLATE == 4) {
-                acc[i][jj][0] += f.a[i][0] ^ f.b[jj][1];
-            } else {
-                acc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[i], f.b[jj], acc[i][jj], 0, 0, 0);
-            }
+    for (int x = 0; x < 32; ++x) {
+        const int i = OZ2_MFMA_ORDER ? (x & 7) : (x >> 2), jj = OZ2_MFMA_ORDER ? (x >> 3) : (x & 3);
+        if (OZ2_ABLATE == 2 || OZ2_ABLATE == 4) {
+            acc[i][jj][0] += f.a[i][0] ^ f.b[jj][1];
+        } else {
+            acc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[i], f.b[jj], acc[i][jj], 0, 0, 0);
         }
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
 }
