@@ -78,7 +78,8 @@ struct GemmArgs {
 #ifndef OZ2_ABLATE
 #define OZ2_ABLATE 0  // probe builds only: 1 = no LDS-DMA, 2 = no MFMA, 3 = no LDS reads, 5 = LDS reads of the first
                      // step only, 6 = LDS-DMA of the prologue only (real operands, no data movement in the loop),
-                     // 7 = residue epilogue reduced to the low byte
+                     // 7 = residue epilogue reduced to the low byte, 8 = every LDS-DMA re-reads k-steps 0/1
+                     // (L2 hits: the fabric / Infinity-Cache share of the DMA)
 #endif
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
     if (OZ2_ABLATE == 1) return;
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     const uint32_t oA = (uint32_t)(((size_t)tm * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
     const uint32_t oB = (uint32_t)(((size_t)tn * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
     auto stage = [&](unsigned ks, unsigned slot) {
-        const size_t go = (size_t)ks * PANEL;
+        const size_t go = (size_t)(OZ2_ABLATE == 8 ? (ks & 1) : ks) * PANEL;  // 8: two k-steps only (all L2 hits)
         const uint32_t lo = lds_wave + slot * SLOT;
         if constexpr (BUF) {
             const uint32_t g32 = (uint32_t)go;
