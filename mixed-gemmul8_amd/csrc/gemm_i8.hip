@@ -3,26 +3,27 @@
 // Replaces the reference's per-modulus hipblasGemmEx + conv_32i_2_8u pair
 // (GEMMul8/src/gemmul8.cu:259-275, conv_32i_2_8u.hpp:7-71): one launch covers all
 // N moduli (grid.y = modulus), each 256x256 output tile accumulates with
-// v_mfma_i32_32x32x32_i8 and is reduced mod p_i in the epilogue, so the int32
+// v_mfma_i32_16x16x64_i8 and is reduced mod p_i in the epilogue, so the int32
 // product never reaches HBM (the reference writes and re-reads 4*m*n bytes per
 // modulus).  The accurate-mode bound product (scaling.hpp:3113-3121) runs the same
 // main loop with a row/column-max epilogue instead of an m x n int32 buffer.
 //
 // Block: 512 threads = 8 waves, two per SIMD, as 2 (M) x 4 (N); each wave owns a
-// 128 x 64 sub-tile = 4 x 2 fragments of 32x32 (128 accumulator registers).
+// 128 x 64 sub-tile = 8 x 4 tiles of 16x16 (128 accumulator registers; the
+// 32x32x32 form, 4 x 2 tiles, remains behind OZ2_MFMA16=0 for A/B probes).
 // The two waves of a SIMD PING-PONG: waves 0-3 (group 0) and 4-7 (group 1) run the
 // same per-k-step sequence
 //     load interval:  12 fragment reads (ds_read_b128, 1 KiB conflict-free sweeps)
 //                     + 4 LDS-DMA pieces of the step D ahead; wait for them
 //     barrier
-//     MFMA interval:  16 MFMAs
+//     MFMA interval:  32 MFMAs (16x16x64; 16 of 32x32x32)
 //     barrier
 // with group 1 one barrier behind, so on every SIMD one wave's MFMAs run while the
 // other wave issues its LDS reads and LDS-DMA (whose issue costs 60-185 cycles each
 // and, with one wave per SIMD, stalled the matrix core).
 // Operand panels (16 KiB, pre-arranged in fragment order by split.hip) stream
-// HBM -> LDS through a 4-slot ring (128 KiB) with global_load_lds issued three
-// k-steps ahead; waits are counted by hand (vmcnt), barriers are raw s_barrier.
+// HBM -> LDS through a 4-slot ring (128 KiB) with LDS-DMA issued three k-steps
+// ahead; waits are counted by hand (vmcnt), barriers are raw s_barrier.
 #include "oz2_split.hpp"
 
 namespace oz2 {
