@@ -81,3 +81,13 @@ def test_log2M_rules():
         assert abs(t["log2M_fast"][N - 2] - (exact - 1.5)) < 1e-5
         assert t["log2M_fast"][N - 2] <= exact - 1.5 + 1e-12
         assert abs(t["log2M_accu"][N - 2] - (exact - 0.5)) < 1e-5
+
+
+def test_tables_compile_as_c_and_cpp(tmp_path):
+    """The same header feeds the C oracle (gcc, C11) and the HIP kernels (C++20): both must parse it."""
+    import subprocess
+    inc = os.path.join(ROOT, "mixed-gemmul8_amd", "csrc", "oz2_tables.inc")
+    src = tmp_path / "t.c"
+    src.write_text('#include "%s"\nint oz2_probe(void) { return oz2_p[1] + (int)oz2_M_hi[0]; }\n' % inc)
+    subprocess.run(["gcc", "-std=c11", "-fsyntax-only", "-Wall", str(src)], check=True)
+    subprocess.run(["g++", "-std=c++20", "-fsyntax-only", "-x", "c++", str(src)], check=True)
