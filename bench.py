@@ -117,14 +117,19 @@ def cpu_baseline(size_hint):
                       f"({os.cpu_count()} logical CPUs visible)"}
 
 
-def traffic_from_profile():
+def traffic_from_profile(shape):
+    """PMC bytes per product launch, from the committed --pmc passes; only for the shape they measured
+    (m, n, k, num_moduli planes per launch, fast mode), else None"""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
-        return json.load(open(p)).get("gemm_hbm_bytes_per_launch")
+        t = json.load(open(p))
     except Exception:
         return None
+    if tuple(t.get("shape", ())) != tuple(shape):
+        return None
+    return t.get("gemm_hbm_bytes_per_launch")
 
 
 def main():
@@ -197,7 +202,7 @@ def main():
         ops = 2.0 * m * n * k * planes
         achieved = ops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(INT8_PEAK_TOPS, 1),
-                    "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4), "traffic": traffic_from_profile(),
+                    "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4), "traffic": traffic_from_profile((m, n, k, planes, not args.accurate)),
                     "kernel": "gemm_i8_kernel<RESIDUE> (int8 ops counted as FLOP, 2*m*n*k*num_moduli per launch)",
                     "avg_launch_ms": round(gemm_ms, 4)}
         # measured live after the timed region: the same MFMA alone on uniformly random operand bytes
