@@ -88,8 +88,12 @@ int gemmul8_recombine(void *stream, size_t m, size_t n, size_t k, unsigned num_m
 void gemmul8_timing_enable(int on);
 int gemmul8_timing_read(double *phase_ms /* [4] */, int *calls);
 
-/* Workspace layout for a shape: fills out[0..15] = {m_pad, n_pad, k_pad, ksteps, planeA, planeB,
- * planeR, offA, offB, offR, offSftA, offSftB, offBound, offSft0, total, kblk}. */
+/* Workspace layout for a shape: fills out[0..23] = {m_pad, n_pad, k_pad, ksteps, planeA, planeB,
+ * planeR, offA, offB, offR, offSftA, offSftB, offBound, offSft0, total, kblk, ldr, nsub, subA, subB,
+ * subR, vsA, vsB, bm_pad}.  Complex compute types run Karatsuba products: per modulus the slice planes
+ * hold the sub-blocks [re | im | re + im] (vsA rows / vsB columns each, subA / subB bytes apart) and the
+ * residue plane the three products Ar Br, Ai Bi, (Ar + Ai)(Br + Bi) (subR bytes apart, ld = ldr);
+ * nsub = 1 otherwise.  The accurate-mode bound maxima are rows [0, bm_pad) then columns. */
 int gemmul8_layout(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, size_t *out);
 
 /* Validation hook: int32 product of plane 0 of the tiled int8 operands already in `work`

@@ -25,7 +25,8 @@ struct CrtArgs {
     const uint8_t *R;
     size_t planeR, ldr;
     size_t m, n;
-    size_t imag_off;  // complex: rows of the imaginary part (= m), else 0
+    size_t imag_off;  // complex big matrix: rows of the imaginary part (= m), else 0
+    size_t sub;       // Karatsuba complex: stride of the sub-planes P1, P2, P3 within a plane
     const int16_t *sftA, *sftB;
     void *C;
     size_t ldc;
@@ -144,12 +145,35 @@ template <> struct BlasEpi<3> {
     }
 };
 
+// Karatsuba complex: the residues of Re = P1 - P2 and Im = P3 - P1 - P2 modulo p_i, for the 8
+// bytes of one load of each sub-plane (byte e of each word); the moduli are compile-time constants.
+template <unsigned N, unsigned... I>
+__device__ __forceinline__ void kara_residues(const uint64_t (&w1)[N], const uint64_t (&w2)[N], const uint64_t (&w3)[N],
+                                              int e, uint8_t (&re)[N], uint8_t (&im)[N],
+                                              std::integer_sequence<unsigned, I...>) {
+    auto one = [&](auto ic) {
+        constexpr unsigned i = decltype(ic)::value;
+        constexpr int p = oz2_p[i];
+        const int b1 = (int)((w1[i] >> (8 * e)) & 0xff), b2 = (int)((w2[i] >> (8 * e)) & 0xff);
+        const int b3 = (int)((w3[i] >> (8 * e)) & 0xff);
+        int r = b1 - b2;
+        r += r < 0 ? p : 0;
+        int t = b3 - b1 - b2;
+        t += t < 0 ? p : 0;
+        t += t < 0 ? p : 0;
+        re[i] = (uint8_t)r;
+        im[i] = (uint8_t)t;
+    };
+    (one(std::integral_constant<unsigned, I>{}), ...);
+}
+
 // One wave covers 512 consecutive rows of a column: lane l recombines rows 8l..8l+7
 // (one 8-byte load per plane), parks the scaled values in LDS, and the wave then
 // writes them back as 16-byte vectors in lane order so the C stream (the larger
 // one) is fully coalesced.  The BLAS epilogue runs after the transpose, on the
-// coalesced C read when beta != 0.
-template <int OT, bool NUMM1, unsigned N>
+// coalesced C read when beta != 0.  KARA (complex outputs): the residues of the real and
+// imaginary parts come from the three Karatsuba sub-planes instead of rows r and r + m.
+template <int OT, bool NUMM1, unsigned N, bool KARA = false>
 __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     using E = typename OutElem<OT>::T;
     constexpr int EPV = 16 / sizeof(E);  // elements per 16-byte vector
@@ -167,7 +191,25 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     E *wb = buf[wv];
     for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
         const int sB = a.sftB[col];
-        if (nr > 0) {
+        if constexpr (KARA) {
+          if (nr > 0) {
+            uint64_t w1[N], w2[N], w3[N];
+            const size_t off = col * a.ldr + r0;
+            load_rows<N>(a, off, nr == CRT_ROWS, nr, w1);
+            load_rows<N>(a, off + a.sub, nr == CRT_ROWS, nr, w2);
+            load_rows<N>(a, off + 2 * a.sub, nr == CRT_ROWS, nr, w3);
+#pragma unroll
+            for (int e = 0; e < CRT_ROWS; ++e) {
+                uint8_t rr[N], ri[N];
+                kara_residues<N>(w1, w2, w3, e, rr, ri, std::make_integer_sequence<unsigned, N>{});
+                const int sft = (int)sa[e] + sB;
+                const double vr = scalbn(crt_value_const<N, NUMM1>(rr, std::make_integer_sequence<unsigned, N>{}), sft);
+                const double vi = scalbn(crt_value_const<N, NUMM1>(ri, std::make_integer_sequence<unsigned, N>{}), sft);
+                if constexpr (OT == 2) wb[lane * CRT_ROWS + e] = make_double2(vr, vi);
+                else if constexpr (OT == 3) wb[lane * CRT_ROWS + e] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
+            }
+          }
+        } else if (nr > 0) {
             uint64_t w[N], wi[N];
             const size_t off = col * a.ldr + r0;
             load_rows<N>(a, off, nr == CRT_ROWS, nr, w);
@@ -228,15 +270,15 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     }
 }
 
-template <int OT, bool NUMM1, unsigned N>
+template <int OT, bool NUMM1, unsigned N, bool KARA>
 static void launch_crt_n(const CrtArgs &a, dim3 grid, hipStream_t st) {
-    crt_kernel<OT, NUMM1, N><<<grid, dim3(256), 0, st>>>(a);
+    crt_kernel<OT, NUMM1, N, KARA><<<grid, dim3(256), 0, st>>>(a);
 }
 
-template <int OT, bool NUMM1>
+template <int OT, bool NUMM1, bool KARA = false>
 static void launch_crt(const CrtArgs &a, unsigned N, dim3 grid, hipStream_t st) {
     switch (N) {
-#define OZ2_N(n) case n: launch_crt_n<OT, NUMM1, n>(a, grid, st); break;
+#define OZ2_N(n) case n: launch_crt_n<OT, NUMM1, n, KARA>(a, grid, st); break;
         OZ2_N(2) OZ2_N(3) OZ2_N(4) OZ2_N(5) OZ2_N(6) OZ2_N(7) OZ2_N(8) OZ2_N(9) OZ2_N(10) OZ2_N(11)
         OZ2_N(12) OZ2_N(13) OZ2_N(14) OZ2_N(15) OZ2_N(16) OZ2_N(17) OZ2_N(18) OZ2_N(19) OZ2_N(20)
 #undef OZ2_N
@@ -249,10 +291,11 @@ void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const i
     CrtArgs a{};
     a.R = R;
     a.planeR = L.planeR;
-    a.ldr = L.m_pad;
+    a.ldr = L.ldr;
     a.m = L.m;
     a.n = L.n;
-    a.imag_off = L.cplx ? L.m : 0;
+    a.imag_off = L.cplx && !L.kara ? L.m : 0;
+    a.sub = L.kara ? L.subR : 0;
     a.sftA = sftA;
     a.sftB = sftB;
     a.C = C;
@@ -276,8 +319,11 @@ void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const i
     switch (ot) {
     case OutType::F64: if (nm1) launch_crt<0, true>(a, CP.N, grid, st); else launch_crt<0, false>(a, CP.N, grid, st); break;
     case OutType::F32: launch_crt<1, true>(a, CP.N, grid, st); break;
-    case OutType::C64: if (nm1) launch_crt<2, true>(a, CP.N, grid, st); else launch_crt<2, false>(a, CP.N, grid, st); break;
-    default: launch_crt<3, true>(a, CP.N, grid, st); break;
+    case OutType::C64:
+        if (L.kara) { if (nm1) launch_crt<2, true, true>(a, CP.N, grid, st); else launch_crt<2, false, true>(a, CP.N, grid, st); }
+        else { if (nm1) launch_crt<2, true>(a, CP.N, grid, st); else launch_crt<2, false>(a, CP.N, grid, st); }
+        break;
+    default: if (L.kara) launch_crt<3, true, true>(a, CP.N, grid, st); else launch_crt<3, true>(a, CP.N, grid, st); break;
     }
 }
 

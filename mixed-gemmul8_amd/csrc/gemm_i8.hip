@@ -71,6 +71,10 @@ struct GemmArgs {
     uint32_t minv[OZ2_MAX_MODULI];   // floor(2^32/p)     (biased unsigned path)
     int bias[OZ2_MAX_MODULI];        // ceil(2^30/p) * p  (accumulator start value, biased path)
     int biased;                      // |product| <= 2^30 (k_pad <= 2^16): biased path
+    // sub-products per modulus (Karatsuba complex: 3, blockIdx.y = 3 j + s), each offset by s times
+    // these strides in the A, B and output planes
+    unsigned nsub;
+    size_t subA, subB, subOut;
 };
 
 // One 16-byte-per-lane LDS-DMA: LDS[m0 + lane*16] <- gsrc (per lane).  Issued from inline asm
@@ -274,7 +278,7 @@ constexpr int ACC_E = 16;
 // every thread of the block must call it: it contains block barriers).
 template <int EPI>
 __device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I][ACC_J], int8_t *smem, int tid, int lane, int wr,
-                                         int wc, unsigned tm, unsigned tn, unsigned j, bool active) {
+                                         int wc, unsigned tm, unsigned tn, unsigned j, unsigned sb, bool active) {
     if constexpr (EPI == (int)Epi::RESIDUE || EPI == EPI_RESIDUE_ADD) {
         const int p = g.p[j];
         uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
@@ -308,7 +312,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I
             park([&](int x) { return residue(x, p, bar, p256); });
         }
         __syncthreads();
-        uint8_t *out = static_cast<uint8_t *>(g.out) + j * g.planeOut + (size_t)tn * 256 * g.ldo + (size_t)tm * 256;
+        uint8_t *out = static_cast<uint8_t *>(g.out) + j * g.planeOut + sb * g.subOut + (size_t)tn * 256 * g.ldo +
+                       (size_t)tm * 256;
 #pragma unroll
         for (int it = 0; it < 4096 / 512; ++it) {
             if (tid >= 512) break;
@@ -381,14 +386,16 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I
 }
 
 // BUF: operand planes below 4 GiB are staged through buffer descriptors (bglds16), larger ones
-// through 64-bit flat addresses (glds16)
-template <int EPI, int BUF>
+// through 64-bit flat addresses (glds16).  SUB: Karatsuba complex, 3 sub-products per modulus
+// (an instantiation of its own, so the real-operand kernel's code is unchanged).
+template <int EPI, int BUF, bool SUB = false>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(1024))) int8_t smem[LDS_BYTES];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;  // wr doubles as the ping-pong group
-    const unsigned j = blockIdx.y;
+    const unsigned j = SUB ? blockIdx.y / 3 : blockIdx.y;  // modulus
+    const unsigned sb = SUB ? blockIdx.y - 3 * j : 0;      // Karatsuba sub-product
 
     // XCD-aware, bijective remap: blocks dealt round-robin over the 8 XCDs get
     // contiguous logical ids per XCD, then a grouped (4 row tiles) raster so the
@@ -403,14 +410,14 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     const unsigned tm = grp * GM + idx % gm, tn = idx / gm;
 
     // LDS-DMA pieces of this wave: 1 KiB blocks {wave, wave + 8} of the A and of the B panel
-    const int8_t *Ag = g.A + j * g.planeA + ((size_t)tm * g.kstride + g.k0) * PANEL + wave * 1024 + lane * 16;
-    const int8_t *Bg = g.B + j * g.planeB + ((size_t)tn * g.kstride + g.k0) * PANEL + wave * 1024 + lane * 16;
+    const int8_t *Ag = g.A + j * g.planeA + sb * g.subA + ((size_t)tm * g.kstride + g.k0) * PANEL + wave * 1024 + lane * 16;
+    const int8_t *Bg = g.B + j * g.planeB + sb * g.subB + ((size_t)tn * g.kstride + g.k0) * PANEL + wave * 1024 + lane * 16;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
     const uint32_t lds_wave = lds_base + wave * 1024;
     const v4si rA = make_rsrc(g.A + j * g.planeA, (uint32_t)g.planeA);
     const v4si rB = make_rsrc(g.B + j * g.planeB, (uint32_t)g.planeB);
-    const uint32_t oA = (uint32_t)(((size_t)tm * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
-    const uint32_t oB = (uint32_t)(((size_t)tn * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
+    const uint32_t oA = (uint32_t)(sb * g.subA + ((size_t)tm * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
+    const uint32_t oB = (uint32_t)(sb * g.subB + ((size_t)tn * g.kstride + g.k0) * PANEL) + wave * 1024 + lane * 16;
     auto stage = [&](unsigned ks, unsigned slot) {
         const size_t go = (size_t)(OZ2_ABLATE == 8 ? (ks & 1) : ks) * PANEL;  // 8: two k-steps only (all L2 hits)
         const uint32_t lo = lds_wave + slot * SLOT;
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     }
     barrier();  // all waves done with the ring before the epilogue reuses it
 
-    epilogue<EPI>(g, acc, smem, tid, lane, wr, wc, tm, tn, j, true);
+    epilogue<EPI>(g, acc, smem, tid, lane, wr, wc, tm, tn, j, sb, true);
 }
 
 
@@ -555,7 +562,13 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     g.ntiles = (unsigned)L.ntiles;
     g.out = out;
     g.planeOut = L.planeR;
-    g.ldo = L.m_pad;
+    g.ldo = L.ldr;
+    // Karatsuba complex: the residue products run as 3 sub-products per modulus; the bound and raw
+    // products always see one (the bound runs on the big-matrix geometry)
+    g.nsub = epi == Epi::RESIDUE ? L.nsub : 1;
+    g.subA = g.nsub > 1 ? L.subA : 0;
+    g.subB = g.nsub > 1 ? L.subB : 0;
+    g.subOut = g.nsub > 1 ? L.subR : 0;
     g.rowmax = rowmax;
     g.colmax = colmax;
     // |int8 product| <= 2^14 * k_pad: the biased residue path needs <= 2^30
@@ -569,11 +582,12 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     }
     g.kstride = g.ksteps;
     g.k0 = 0;
-    dim3 grid((unsigned)(L.mtiles * L.ntiles), nplanes);
+    dim3 grid((unsigned)(L.mtiles * L.ntiles), nplanes * g.nsub);
     // GEMMUL8_FORCE_FLAT_DMA=1 takes the 64-bit path at any size (tests cover it with small shapes)
     const char *ff = getenv("GEMMUL8_FORCE_FLAT_DMA");
     const bool buf = L.planeA < ((size_t)1 << 32) && L.planeB < ((size_t)1 << 32) && !(ff && atoi(ff));
-#define OZ2_GEMM(E, B) gemm_i8_kernel<E, B><<<grid, dim3(NTHREADS), 0, st>>>(g)
+#define OZ2_GEMM1(E, B) gemm_i8_kernel<E, B><<<grid, dim3(NTHREADS), 0, st>>>(g)
+#define OZ2_GEMM(E, B) (g.nsub == 3 ? (void)(gemm_i8_kernel<E, B, true><<<grid, dim3(NTHREADS), 0, st>>>(g)) : (void)OZ2_GEMM1(E, B))
     // beyond k_pad = 2^17 an int32 product can wrap (the reference's int32 C32i does): the residue
     // product then runs in k-chunks of 2^16 (biased path), each adding its residues into the planes
     // mod p.  GEMMUL8_KCHUNK (k-steps, multiple of 1) forces chunking at small k for the tests.
@@ -594,10 +608,11 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     }
     switch (epi) {
     case Epi::RESIDUE: buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0); break;
-    case Epi::BOUND: buf ? OZ2_GEMM(1, 1) : OZ2_GEMM(1, 0); break;
-    default: buf ? OZ2_GEMM(2, 1) : OZ2_GEMM(2, 0); break;
+    case Epi::BOUND: buf ? OZ2_GEMM1(1, 1) : OZ2_GEMM1(1, 0); break;
+    default: buf ? OZ2_GEMM1(2, 1) : OZ2_GEMM1(2, 0); break;
     }
 #undef OZ2_GEMM
+#undef OZ2_GEMM1
 }
 
 }  // namespace oz2

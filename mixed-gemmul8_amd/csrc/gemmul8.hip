@@ -211,7 +211,8 @@ static ModParams sub_mod_params(unsigned N, unsigned j0, unsigned j1) {
 // accurate mode, first half of phase 1: sft0 = 5 - ilogb(amax), the 6-bit magnitude planes and the
 // bound product's row / column maxima (scaling.hpp:3053-3100).  A on the call's stream, B on the lane.
 static void phase_bound(const Call &c, const Views &v) {
-    const Layout &L = v.L;
+    // always the big-matrix geometry (Karatsuba layouts size their slice regions to hold it)
+    const Layout L = v.L.kara ? make_layout(c.m, c.n, c.k, c.N, c.cplx, v.L.S, 0) : v.L;
     const ModParams MP = make_mod_params(c.N);
     fork(c);
     split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
@@ -237,7 +238,7 @@ static void operand_shifts(const Call &c, const Views &v, bool is_A, hipStream_t
     } else {
         const float log2M = oz2_log2M_accu[c.N - 2];
         if (is_A) split_finalize_accurate(v.sft0, v.bound, c.m, log2M, v.sftA, st, c.cplx);
-        else split_finalize_accurate(v.sft0 + L.m_pad, v.bound + L.m_pad, c.n, log2M, v.sftB, st);
+        else split_finalize_accurate(v.sft0 + L.bm_pad, v.bound + L.bm_pad, c.n, log2M, v.sftB, st);
     }
 }
 
@@ -442,7 +443,7 @@ int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, si
     if (m == 0 && n == 0) return GEMMUL8_OK;
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, c.cplx);
     if (m == 0 || n == 0) {  // an empty block contributes nothing to the other operand's maxima
-        oz2::zero_i32(v.bound, v.L.m_pad + v.L.n_pad, c.st);
+        oz2::zero_i32(v.bound, v.L.bm_pad + v.L.bn_pad, c.st);
         return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
     }
     oz2::LaneGuard lane(c);
@@ -529,9 +530,10 @@ int gemmul8_timing_read(double *phase_ms, int *calls) {
 
 int gemmul8_layout(size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, size_t *out) {
     const oz2::Layout L = oz2::make_layout(m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
-    const size_t v[16] = {L.m_pad, L.n_pad, L.k_pad, L.ksteps, L.planeA, L.planeB, L.planeR, L.offA,
-                          L.offB, L.offR, L.offSftA, L.offSftB, L.offBound, L.offSft0, L.total, L.kblk};
-    for (int i = 0; i < 16; ++i) out[i] = v[i];
+    const size_t v[24] = {L.m_pad, L.n_pad, L.k_pad,  L.ksteps, L.planeA, L.planeB, L.planeR, L.offA,
+                          L.offB,  L.offR,  L.offSftA, L.offSftB, L.offBound, L.offSft0, L.total, L.kblk,
+                          L.ldr,   L.nsub,  L.subA,  L.subB,   L.subR,   L.vsA,    L.vsB,    L.bm_pad};
+    for (int i = 0; i < 24; ++i) out[i] = v[i];
     return GEMMUL8_OK;
 }
 

@@ -20,6 +20,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #ifndef OCML_BASIC_ROUNDED_OPERATIONS
 #error "build with -DOCML_BASIC_ROUNDED_OPERATIONS (directed-rounding intrinsics)"
@@ -41,45 +42,93 @@ struct Layout {
     unsigned N;
     bool cplx;
     // int8 product shape
-    size_t mr, kr;       // rows of the int8 A (m or 2m), k-extent incl. complex blocks
-    size_t kblk;         // k padded to KSTEP (offset of the imaginary block for complex)
+    size_t mr, kr;       // rows of the int8 A (m, 2m big matrix, 3 m_s Karatsuba), k-extent incl. complex blocks
+    size_t kblk;         // k padded to KSTEP (offset of the imaginary block of the big-matrix encode)
     size_t m_pad, n_pad, k_pad;
-    size_t ksteps, mtiles, ntiles;
+    size_t ksteps, mtiles, ntiles;  // tiles of ONE sub-product
     size_t planeA, planeB, planeR;  // bytes per modulus
-    unsigned S;                     // slice planes held at once (= N unless low-memory mode)
+    size_t ldr;                     // leading dimension of a residue (sub-)plane
+    // Karatsuba complex products (kara): per modulus three sub-products of the sub-blocks
+    // [re | im | re + im] of A's rows and of B's columns, P1 = Ar Br, P2 = Ai Bi, P3 = (Ar+Ai)(Br+Bi):
+    // 3 m n k MACs instead of the big matrix's 4 m n k.  The CRT combines their residues into
+    // Re = P1 - P2 and Im = P3 - P1 - P2 (mod p).  Otherwise nsub = 1 and the sub strides are 0.
+    bool kara;
+    unsigned nsub;
+    size_t subA, subB, subR;  // byte stride between the sub-blocks of a slice plane / residue plane
+    size_t vsA, vsB;          // vectors per sub-block (m and n rounded up to TILE)
+    // accurate-mode bound product: always the big-matrix geometry (the reference's bound, quirks
+    // included); its row / column maxima and sft0 are indexed with these extents
+    size_t bm_pad, bn_pad;
+    unsigned S;                    // slice planes held at once (= N unless low-memory mode)
     // workspace offsets (bytes)
     size_t offA, offB, offR, offSftA, offSftB, offBound, offSft0, total;
 };
 
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+// Complex products as Karatsuba sub-products (default) or as the reference's big matrix
+// (GEMMUL8_CPLX_BIGMATRIX=1: A/B runs and the tests of the big-matrix planes).  The residues of
+// Re(AB) and Im(AB) mod p, hence C, are the same bits either way.
+static inline bool kara_default() {
+    static const bool big = [] {
+        const char *e = getenv("GEMMUL8_CPLX_BIGMATRIX");
+        return e && atoi(e) != 0;
+    }();
+    return !big;
+}
+
 // slice_planes: planes of A / B slices held at once (N: all resident; fewer: the low-memory
 // mode encodes the moduli in groups of that size into the same planes, gemmul8.hip run())
-static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool cplx, unsigned slice_planes = 0) {
+// kara: -1 = kara_default() for complex, 0 = the big-matrix geometry (the accurate-mode bound)
+static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool cplx, unsigned slice_planes = 0,
+                                 int kara = -1) {
     Layout L{};
     const unsigned S = (slice_planes == 0 || slice_planes > N) ? N : slice_planes;
     L.S = S;
     L.m = m; L.n = n; L.k = k; L.N = N; L.cplx = cplx;
     L.kblk = round_up(k, KSTEP);
+    // big-matrix geometry (real operands: the only one)
     L.mr = cplx ? 2 * m : m;
     L.kr = cplx ? 2 * L.kblk : L.kblk;
     L.m_pad = round_up(L.mr, TILE);
     L.n_pad = round_up(n, TILE);
     L.k_pad = L.kr;
+    L.bm_pad = L.m_pad;
+    L.bn_pad = L.n_pad;
+    const size_t big_planeA = L.m_pad * L.k_pad, big_planeB = L.n_pad * L.k_pad;
+    L.kara = cplx && (kara < 0 ? kara_default() : kara != 0);
+    L.nsub = 1;
+    if (L.kara) {
+        L.vsA = round_up(m, TILE);
+        L.vsB = round_up(n, TILE);
+        L.nsub = 3;
+        L.mr = 3 * L.vsA;
+        L.kr = L.kblk;
+        L.m_pad = L.mr;
+        L.n_pad = 3 * L.vsB;
+        L.k_pad = L.kblk;
+        L.subA = L.vsA * L.k_pad;
+        L.subB = L.vsB * L.k_pad;
+        L.subR = L.vsA * L.vsB;
+    }
     L.ksteps = L.k_pad / KSTEP;
-    L.mtiles = L.m_pad / TILE;
-    L.ntiles = L.n_pad / TILE;
+    L.mtiles = (L.kara ? L.vsA : L.m_pad) / TILE;
+    L.ntiles = (L.kara ? L.vsB : L.n_pad) / TILE;
     L.planeA = L.m_pad * L.k_pad;
     L.planeB = L.n_pad * L.k_pad;
-    L.planeR = L.m_pad * L.n_pad;
+    L.ldr = L.kara ? L.vsA : L.m_pad;
+    L.planeR = L.kara ? 3 * L.subR : L.m_pad * L.n_pad;
+    // the slice regions also hold the bound product's big-matrix magnitude plane (accurate mode)
+    const size_t regA = L.planeA * S > big_planeA ? L.planeA * S : big_planeA;
+    const size_t regB = L.planeB * S > big_planeB ? L.planeB * S : big_planeB;
     size_t off = 0;
-    L.offA = off; off += round_up(L.planeA * S, 256);
-    L.offB = off; off += round_up(L.planeB * S, 256);
+    L.offA = off; off += round_up(regA, 256);
+    L.offB = off; off += round_up(regB, 256);
     L.offR = off; off += round_up(L.planeR * N, 256);
-    L.offSftA = off; off += round_up(L.m_pad * 2, 256);
-    L.offSftB = off; off += round_up(L.n_pad * 2, 256);
-    L.offBound = off; off += round_up((L.m_pad + L.n_pad) * 4, 256);
-    L.offSft0 = off; off += round_up((L.m_pad + L.n_pad) * 2, 256);
+    L.offSftA = off; off += round_up(L.bm_pad * 2, 256);
+    L.offSftB = off; off += round_up(L.bn_pad * 2, 256);
+    L.offBound = off; off += round_up((L.bm_pad + L.bn_pad) * 4, 256);
+    L.offSft0 = off; off += round_up((L.bm_pad + L.bn_pad) * 2, 256);
     L.total = off;
     return L;
 }

@@ -20,7 +20,17 @@
 
 namespace oz2 {
 
-enum : int { ENC_CONJ = 1, ENC_BTAIL = 2, ENC_KFIRST = 4 };
+enum : int { ENC_CONJ = 1, ENC_BTAIL = 2, ENC_KFIRST = 4, ENC_KARA = 8 };
+
+// (a + b) mod p as the symmetric representative of an int8 slice, for residues a, b of mod_8i
+// (|a|, |b| <= p/2; p = 256: any byte of a + b is the residue)
+__device__ __forceinline__ int center_sum(int a, int b, int p) {
+    const int h = (p - 1) >> 1;
+    int s = a + b;
+    s -= s > h ? p : 0;
+    s += s < -h ? p : 0;
+    return s;
+}
 #ifndef OZ2_ENC_ABLATE
 #define OZ2_ENC_ABLATE 0  // probe builds only (tools/probes/enc_probe.hip)
 #endif
@@ -368,10 +378,16 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
     }
 
     const bool top = v < nvec || !CPLX || !IS_A;  // complex A: rows >= m only emit their (zero) bottom copy
-    // one plane of slices: real -> (v, kk); complex A -> [wr, -wi] / [wi, wr]; complex B -> [wr; wi]
-    auto emit = [&](int8_t *o, const uint32_t (&wr)[4], const uint32_t (&wi)[4]) {
+    const bool kara = CPLX && (flags & ENC_KARA) != 0;
+    // one plane of slices: real -> (v, kk); complex A -> [wr, -wi] / [wi, wr]; complex B -> [wr; wi];
+    // Karatsuba (either operand): vectors v, v + vmax, v + 2 vmax <- wr, wi, ws = (wr + wi) mod p
+    auto emit = [&](int8_t *o, const uint32_t (&wr)[4], const uint32_t (&wi)[4], const uint32_t (&ws)[4]) {
         if (!CPLX) {
             *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+        } else if (kara) {
+            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+            *reinterpret_cast<uint4 *>(o + panel_offset(v + vmax, kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
+            *reinterpret_cast<uint4 *>(o + panel_offset(v + 2 * vmax, kk, ksteps)) = make_uint4(ws[0], ws[1], ws[2], ws[3]);
         } else if (IS_A) {
             // -im as bytes: per-byte two's complement negation
             uint32_t ni[4];
@@ -421,9 +437,24 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
             wr[d] = ar;
             wi[d] = ai;
         }
-        emit(out, wr, wi);
+        emit(out, wr, wi, wi);
         return;
     }
+
+    // Karatsuba sum plane from the two slices as stored (int8), whatever their representatives
+    // (the f32 path's mod_8i<float> steps are not always the symmetric residue above N = 10)
+    auto sum_words = [&](const int (&rr)[16], const int (&ri)[16], int p, uint32_t (&ws)[4]) {
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+            uint32_t a = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int s = ((int)(int8_t)rr[4 * d + b] + (int)(int8_t)ri[4 * d + b]) % p;  // (-p, p)
+                a |= ((uint32_t)center_sum(s, 0, p) & 0xffu) << (8 * b);
+            }
+            ws[d] = a;
+        }
+    };
 
     // one plane: residues of the 16 elements from their f32 reductions t modulo P (one step of
     // the tail of mod_8i, scaling.hpp:218-222, on packed pairs) -> bytes -> emit
@@ -461,7 +492,9 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
             wr[d] = ar;
             wi[d] = ai;
         }
-        emit(out + (size_t)j * plane, wr, wi);
+        uint32_t ws[4] = {0, 0, 0, 0};
+        if (kara) sum_words(rr, ri, p, ws);
+        emit(out + (size_t)j * plane, wr, wi, ws);
     };
 
     // Pair form (one f32 step per modulus) straight to bytes.  With C = 1.5*2^23 and tc = t + C
@@ -470,10 +503,28 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
     // pattern carries the residue in its low byte (two's complement, as the int8 cast of mod_8i
     // stores it).  Three packed ops per pair and three byte permutes per four bytes replace the
     // multiply / round / fma, the f32 -> i32 conversion and the shift-or packing.
+    // Karatsuba: the sum plane from ts = tr + ti (exact, |ts| <= P < 2^16, so the same one step is exact)
     auto plane_bytes = [&](unsigned j, const float (&tr)[16], const float (&trc)[16], const float (&ti)[16],
-                           const float (&tic)[16]) {
+                           const float (&tic)[16], const float (&ts)[16], const float (&tsc)[16]) {
         const float rf = MP.rinv_f[j];
         const f2v C2 = {12582912.0f, 12582912.0f}, r2 = {rf, rf}, q2 = {-(float)MP.p[j], -(float)MP.p[j]};
+        uint32_t ws[4] = {0, 0, 0, 0};
+        if (kara) {
+            uint32_t bs[16];
+#pragma unroll
+            for (int q = 0; q < 16; q += 2) {
+                const f2v y = __builtin_elementwise_fma(f2v{ts[q], ts[q + 1]}, r2, C2) - C2;
+                const f2v a = __builtin_elementwise_fma(y, q2, f2v{tsc[q], tsc[q + 1]});
+                bs[q] = __float_as_uint(a.x);
+                bs[q + 1] = __float_as_uint(a.y);
+            }
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t lo = __builtin_amdgcn_perm(bs[4 * d + 1], bs[4 * d], 0x0c0c0400u);
+                const uint32_t hi = __builtin_amdgcn_perm(bs[4 * d + 3], bs[4 * d + 2], 0x0c0c0400u);
+                ws[d] = __builtin_amdgcn_perm(hi, lo, 0x05040100u);
+            }
+        }
         uint32_t br[16], bi[16];
 #pragma unroll
         for (int q = 0; q < 16; q += 2) {
@@ -503,7 +554,7 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                 wi[d] = 0;
             }
         }
-        emit(out + (size_t)j * plane, wr, wi);
+        emit(out + (size_t)j * plane, wr, wi, ws);
     };
 
     // integer-valued f64 values -> group reductions -> planes
@@ -517,13 +568,15 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                 tim[q] = CPLX ? __double2float_rn(__builtin_fma(__builtin_rint(di[q] * rP), -P, di[q])) : 0.0f;
             }
             if (G.steps == 1 && G.bytes && OZ2_ENC_ABLATE == 0) {
-                float trc[16], tic[16];
+                float trc[16], tic[16], ts[16], tsc[16];
 #pragma unroll
                 for (int q = 0; q < 16; ++q) {
                     trc[q] = tr[q] + 12582912.0f;
                     tic[q] = tim[q] + 12582912.0f;
+                    ts[q] = kara ? tr[q] + tim[q] : 0.0f;
+                    tsc[q] = ts[q] + 12582912.0f;
                 }
-                for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_bytes((unsigned)j, tr, trc, tim, tic);
+                for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_bytes((unsigned)j, tr, trc, tim, tic, ts, tsc);
             } else if (G.steps == 1) {
                 for (int j = G.start[gi]; j < G.start[gi + 1]; ++j) plane_from.template operator()<1>((unsigned)j, tr, tim);
             } else {
@@ -567,7 +620,9 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                 wr[d] = ar;
                 wi[d] = ai;
             }
-            emit(out + (size_t)j * plane, wr, wi);
+            uint32_t ws[4] = {0, 0, 0, 0};
+            if (kara) sum_words(rr, ri, p, ws);
+            emit(out + (size_t)j * plane, wr, wi, ws);
         }
     }
 }
@@ -657,12 +712,15 @@ void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool acc
 
 void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
                   size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st, bool btail_quirk) {
-    const int flags = (d.conj ? ENC_CONJ : 0) | (btail_quirk && mode == 1 && !is_A ? ENC_BTAIL : 0);
+    const bool kara = L.kara && mode == 0;  // (the accurate-mode bound is encoded as the big matrix)
+    const int flags = (d.conj ? ENC_CONJ : 0) | (btail_quirk && mode == 1 && !is_A ? ENC_BTAIL : 0) |
+                      (kara ? ENC_KARA : 0);
     // grid extent over vectors: padded rows/cols get zero slices; complex A covers
-    // [0, m_pad - m) so that rows [2m, m_pad) are zeroed through their bottom copy
-    size_t vpad = is_A ? (d.cplx ? L.m_pad - L.m : L.m_pad) : L.n_pad;
+    // [0, m_pad - m) so that rows [2m, m_pad) are zeroed through their bottom copy; Karatsuba
+    // covers one sub-block, each vector emitting its three copies (vmax = the sub-block stride)
+    size_t vpad = kara ? (is_A ? L.vsA : L.vsB) : is_A ? (d.cplx ? L.m_pad - L.m : L.m_pad) : L.n_pad;
     vpad = round_up(vpad, 64);
-    const size_t vmax = is_A ? L.m_pad : L.n_pad;
+    const size_t vmax = kara ? (is_A ? L.vsA : L.vsB) : is_A ? L.m_pad : L.n_pad;
 #define OZ2_LE(R, C, A) launch_encode<R, C, A>(d.ptr, d.ld, d.contig, nvec, len, sft, out, plane, L, vpad, vmax, mode, flags, MP, st)
     if (d.dbl) {
         if (d.cplx) { if (is_A) OZ2_LE(double, true, true); else OZ2_LE(double, true, false); }

@@ -90,10 +90,11 @@ def workSize(m, n, k, num_moduli, computeType=REAL_DEFAULT, slice_planes=None):
 
 
 def layout(m, n, k, num_moduli, computeType=REAL_DEFAULT):
-    out = (ctypes.c_size_t * 16)()
+    out = (ctypes.c_size_t * 24)()
     lib.gemmul8_layout(m, n, k, num_moduli, computeType, out)
     keys = ["m_pad", "n_pad", "k_pad", "ksteps", "planeA", "planeB", "planeR", "offA", "offB", "offR", "offSftA",
-            "offSftB", "offBound", "offSft0", "total", "kblk"]
+            "offSftB", "offBound", "offSft0", "total", "kblk", "ldr", "nsub", "subA", "subB", "subR", "vsA", "vsB",
+            "bm_pad"]
     return dict(zip(keys, list(out)))
 
 
@@ -141,7 +142,7 @@ def split_bound(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, work, out_dtype, 
     L = layout(m, n, k, num_moduli, computeType)
     o = L["offBound"]
     rowmax = work[o:o + 4 * m].view(torch.int32)
-    colmax = work[o + 4 * L["m_pad"]:o + 4 * L["m_pad"] + 4 * n].view(torch.int32)
+    colmax = work[o + 4 * L["bm_pad"]:o + 4 * L["bm_pad"] + 4 * n].view(torch.int32)
     return rowmax, colmax
 
 

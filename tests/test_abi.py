@@ -67,6 +67,26 @@ def test_work_size_and_errors_host_only():
     assert lib.gemmul8_gemm(*args(14, k=(1 << 19) - 63, fast=0)) == -4  # accurate: int32 bound product
 
 
+def test_complex_karatsuba_layout():
+    """complex compute types run Karatsuba sub-products (3 per modulus, csrc/oz2_common.hpp); the
+    workspace also holds the accurate-mode big-matrix bound plane; real layouts are unchanged"""
+    if os.environ.get("GEMMUL8_CPLX_BIGMATRIX"):
+        return
+    import gemmul8 as G
+    for m, n, k in ((70, 90, 333), (300, 5, 64), (4096, 4096, 4096)):
+        L = G.layout(m, n, k, 12, G.COMPLEX_BIG_MATRIX_ENCODE)
+        assert L["nsub"] == 3 and L["vsA"] == -(-m // 256) * 256 and L["vsB"] == -(-n // 256) * 256
+        assert L["planeR"] == 3 * L["subR"] == 3 * L["vsA"] * L["vsB"] and L["ldr"] == L["vsA"]
+        kb = -(-k // 64) * 64
+        assert L["planeA"] == 3 * L["vsA"] * kb and L["subA"] == L["vsA"] * kb and L["subB"] == L["vsB"] * kb
+        assert L["offB"] - L["offA"] >= max(12 * L["planeA"], L["bm_pad"] * 2 * kb)
+        assert L["offR"] - L["offB"] >= max(12 * L["planeB"], -(-n // 256) * 256 * 2 * kb)
+        assert L["bm_pad"] == -(-2 * m // 256) * 256
+        assert G.workSize(m, n, k, 12, G.COMPLEX_BIG_MATRIX_ENCODE) == L["total"]
+        R = G.layout(m, n, k, 12, G.REAL_DEFAULT)
+        assert R["nsub"] == 1 and R["ldr"] == R["m_pad"] and R["planeR"] == R["m_pad"] * R["n_pad"]
+
+
 def test_interposer_exports_and_has_no_runtime_dependency():
     """libgemmul8_hijack.so: the intercepted hipBLAS / rocBLAS GEMM symbols, and no link-time HIP
     or BLAS dependency (a second HIP runtime in a framework process would break it)."""

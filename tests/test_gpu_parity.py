@@ -7,10 +7,15 @@ Bit-exact expectations (integer / exactly restated arithmetic):
   * every residue plane (the int8 products are exact),
   * C bit-for-bit for f64/f32/complex outputs.
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 
 from util import bits_equal, randmat_np, untile
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
 
 pytestmark = pytest.mark.gpu
 
@@ -82,6 +87,11 @@ def check_full(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta
     agree_A = float(np.mean(sA == sAo)) if m else 1.0
     agree_B = float(np.mean(sB == sBo)) if n else 1.0
     assert agree_A == 1.0 and agree_B == 1.0, (agree_A, agree_B, np.nonzero(sA != sAo), np.nonzero(sB != sBo))
+    Co = O.gemm(A, B, N, fast, out_dtype, alpha, beta, C0, opA, opB, vt, ctype=ctype)
+    if L["nsub"] == 3:  # Karatsuba complex products: planes derived from the oracle's big matrix
+        check_kara_planes(wsb, L, N, m, n, k, A8o, B8o)
+        assert bits_equal(C, Co), f"C mismatch: max |diff| {np.max(np.abs(C - Co))}"
+        return C, Co
     # slices (with the complex imaginary block at kblk instead of k) and zero padding
     kblk = L["kblk"]
     for which, X8o, vpad, nv in (("A", A8o, L["m_pad"], (2 * m if cplx else m)), ("B", B8o, L["n_pad"], n)):
@@ -99,9 +109,54 @@ def check_full(A, B, N, fast=True, opA=0, opB=0, out_dtype=None, alpha=1.0, beta
     Ro = O.residues(A8o, B8o)
     mr = 2 * m if cplx else m
     assert np.array_equal(R[:, :n, :mr], Ro), "residue mismatch"
-    Co = O.gemm(A, B, N, fast, out_dtype, alpha, beta, C0, opA, opB, vt, ctype=ctype)
     assert bits_equal(C, Co), f"C mismatch: max |diff| {np.max(np.abs(C - Co))}"
     return C, Co
+
+
+def _center(x, p):
+    """symmetric representative of x mod p as the int8 byte the encoder stores"""
+    r = np.mod(x, p)
+    r = np.where(r > (p - 1) // 2, r - p, r)
+    return r.astype(np.int64).astype(np.int8)
+
+
+def check_kara_planes(wsb, L, N, m, n, k, A8o, B8o):
+    """Karatsuba layout (csrc/oz2_common.hpp): per modulus, slice sub-blocks [re | im | re + im] of
+    vsA rows / vsB columns, and residue sub-planes Ar Br, Ai Bi, (Ar + Ai)(Br + Bi) mod p.  The
+    oracle's big-matrix slices hold Ar = A8[:m, :k], Ai = A8[m:, :k], Br = B8[:, :k], Bi = B8[:, k:]
+    (scaling.hpp:753-838, 1150-1230); its residues Re(AB) = rows [0, m), Im(AB) = rows [m, 2m)."""
+    from gen_tables import MODULI
+    vsA, vsB, kp = L["vsA"], L["vsB"], L["k_pad"]
+    Ro = None
+    Rw = wsb[L["offR"]:L["offR"] + N * L["planeR"]].reshape(N, 3, vsB, vsA)
+    for j in range(N):
+        p = MODULI[j]
+        Ar, Ai = A8o[j][:m, :k].astype(np.int64), A8o[j][m:2 * m, :k].astype(np.int64)
+        Br, Bi = B8o[j][:, :k].astype(np.int64), B8o[j][:, k:].astype(np.int64)
+        for which, (Xr, Xi), vs, off, plane in (("A", (Ar, Ai), vsA, L["offA"], L["planeA"]),
+                                                ("B", (Br, Bi), vsB, L["offB"], L["planeB"])):
+            P = untile(wsb[off + j * plane: off + (j + 1) * plane].tobytes(), 3 * vs, kp)
+            exp = np.zeros((3 * vs, kp), np.int8)
+            nv = Xr.shape[0]
+            exp[:nv, :k] = Xr
+            exp[vs:vs + nv, :k] = Xi
+            exp[2 * vs:2 * vs + nv, :k] = _center(Xr + Xi, p)
+            assert np.array_equal(P, exp), f"{which} Karatsuba slice mismatch modulus {j}: {np.argwhere(P != exp)[:5]}"
+        S_A, S_B = _center(Ar + Ai, p).astype(np.int64), _center(Br + Bi, p).astype(np.int64)
+        for s, (X, Y) in enumerate(((Ar, Br), (Ai, Bi), (S_A, S_B))):
+            exp = np.mod(Y @ X.T, p).astype(np.uint8)  # [col][row]
+            got = Rw[j, s, :n, :m]
+            assert np.array_equal(got, exp), f"Karatsuba residue mismatch modulus {j} sub-product {s}"
+        if Ro is None:
+            Ro = O_residues(A8o, B8o)
+        re = np.mod(Rw[j, 0, :n, :m].astype(np.int64) - Rw[j, 1, :n, :m], p)
+        im = np.mod(Rw[j, 2, :n, :m].astype(np.int64) - Rw[j, 0, :n, :m] - Rw[j, 1, :n, :m], p)
+        assert np.array_equal(re, Ro[j][:, :m]) and np.array_equal(im, Ro[j][:, m:2 * m]), f"Re/Im residues modulus {j}"
+
+
+def O_residues(A8o, B8o):
+    from oracle import oracle as O
+    return O.residues(A8o, B8o)
 
 
 @pytest.mark.parametrize("m,n,k", [(16, 16, 16), (33, 47, 100), (256, 256, 256), (300, 260, 513), (1, 1, 1)])
@@ -312,6 +367,30 @@ def test_k_chunks_forced(fast):
     tdir = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(tdir)
     env = dict(os.environ, GEMMUL8_KCHUNK="2")
+    r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
+
+
+def test_complex_big_matrix_products():
+    """GEMMUL8_CPLX_BIGMATRIX=1 (child process): complex products as the reference's big matrix
+    (one 2m x n x 2k product per modulus) instead of the Karatsuba sub-products; slices, residue
+    planes and C against the oracle, fast and accurate, all three compute types, ops N/T/C"""
+    import subprocess
+    code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
+            "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
+            "import gemmul8 as G\n"
+            "rng = np.random.default_rng(11)\n"
+            "L = G.layout(70, 90, 333, 9, G.COMPLEX_BIG_MATRIX_ENCODE)\n"
+            "assert L['nsub'] == 1, L\n"
+            "for ct in (1, 2, 3):\n"
+            "    check_full(randmat_np(rng, 70, 333, dtype=np.complex128), randmat_np(rng, 333, 90, dtype=np.complex128), 12, ctype=ct)\n"
+            "    check_full(randmat_np(rng, 41, 62, dtype=np.complex128), randmat_np(rng, 62, 35, dtype=np.complex128), 12, fast=False, ctype=ct)\n"
+            "check_full(randmat_np(rng, 50, 33, dtype=np.complex64), randmat_np(rng, 40, 50, dtype=np.complex64), 7, opA=2, opB=1)\n"
+            "print('OK')")
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    env = dict(os.environ, GEMMUL8_CPLX_BIGMATRIX="1")
     r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
