@@ -66,20 +66,30 @@ struct Layout {
 
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Complex products as Karatsuba sub-products (default) or as the reference's big matrix
-// (GEMMUL8_CPLX_BIGMATRIX=1: A/B runs and the tests of the big-matrix planes).  The residues of
-// Re(AB) and Im(AB) mod p, hence C, are the same bits either way.
-static inline bool kara_default() {
-    static const bool big = [] {
-        const char *e = getenv("GEMMUL8_CPLX_BIGMATRIX");
-        return e && atoi(e) != 0;
+// Complex products as Karatsuba sub-products or as the reference's big matrix.  The residues of
+// Re(AB) and Im(AB) mod p, hence C, are the same bits either way.  Karatsuba saves a quarter of
+// the MACs but reads a third residue plane per modulus in the CRT, writes a third B sub-block,
+// and halves the k-steps per product block (whose fixed cost then weighs twice as much); measured
+// on MI355X (tools/probes/kara_sweep.py, N = 12, Karatsuba / big-matrix time): 4096^3 0.87,
+// 3072^3 0.92, 4096 x 256 x 4096 0.89; 2048^3 0.97-1.00, 1536^3 1.00-1.04, 1024^3 1.07,
+// 8192^2 x 1024 1.07, 256 x 4096 x 4096 1.13.  Hence the rule below.
+// GEMMUL8_CPLX_PRODUCTS=karatsuba / bigmatrix forces either (tests, A/B runs).
+static inline bool kara_default(size_t m, size_t n, size_t k) {
+    static const int forced = [] {
+        const char *e = getenv("GEMMUL8_CPLX_PRODUCTS");
+        if (!e) return 0;
+        if (e[0] == 'k') return 1;
+        if (e[0] == 'b') return 2;
+        return 0;
     }();
-    return !big;
+    if (forced) return forced == 1;
+    (void)n;
+    return k >= 3072 && m >= 1024;
 }
 
 // slice_planes: planes of A / B slices held at once (N: all resident; fewer: the low-memory
 // mode encodes the moduli in groups of that size into the same planes, gemmul8.hip run())
-// kara: -1 = kara_default() for complex, 0 = the big-matrix geometry (the accurate-mode bound)
+// kara: -1 = kara_default(m, n, k) for complex, 0 = the big-matrix geometry (the accurate-mode bound)
 static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool cplx, unsigned slice_planes = 0,
                                  int kara = -1) {
     Layout L{};
@@ -96,7 +106,7 @@ static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool 
     L.bm_pad = L.m_pad;
     L.bn_pad = L.n_pad;
     const size_t big_planeA = L.m_pad * L.k_pad, big_planeB = L.n_pad * L.k_pad;
-    L.kara = cplx && (kara < 0 ? kara_default() : kara != 0);
+    L.kara = cplx && (kara < 0 ? kara_default(m, n, k) : kara != 0);
     L.nsub = 1;
     if (L.kara) {
         L.vsA = round_up(m, TILE);

@@ -70,10 +70,14 @@ def test_work_size_and_errors_host_only():
 def test_complex_karatsuba_layout():
     """complex compute types run Karatsuba sub-products (3 per modulus, csrc/oz2_common.hpp); the
     workspace also holds the accurate-mode big-matrix bound plane; real layouts are unchanged"""
-    if os.environ.get("GEMMUL8_CPLX_BIGMATRIX"):
+    if os.environ.get("GEMMUL8_CPLX_PRODUCTS"):
         return
     import gemmul8 as G
-    for m, n, k in ((70, 90, 333), (300, 5, 64), (4096, 4096, 4096)):
+    # the size rule (oz2_common.hpp kara_default): Karatsuba from k >= 3072 and m >= 1024
+    for m, n, k in ((70, 90, 333), (1024, 1024, 1024), (2048, 2048, 2048), (256, 4096, 4096), (8192, 8192, 1024)):
+        L = G.layout(m, n, k, 12, G.COMPLEX_BIG_MATRIX_ENCODE)
+        assert L["nsub"] == 1 and L["m_pad"] == L["bm_pad"] == -(-2 * m // 256) * 256 and L["ldr"] == L["m_pad"]
+    for m, n, k in ((3072, 3072, 3072), (4096, 256, 4096), (4096, 4096, 4096)):
         L = G.layout(m, n, k, 12, G.COMPLEX_BIG_MATRIX_ENCODE)
         assert L["nsub"] == 3 and L["vsA"] == -(-m // 256) * 256 and L["vsB"] == -(-n // 256) * 256
         assert L["planeR"] == 3 * L["subR"] == 3 * L["vsA"] * L["vsB"] and L["ldr"] == L["vsA"]

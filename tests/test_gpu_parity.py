@@ -372,25 +372,40 @@ def test_k_chunks_forced(fast):
     assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
 
 
-def test_complex_big_matrix_products():
-    """GEMMUL8_CPLX_BIGMATRIX=1 (child process): complex products as the reference's big matrix
-    (one 2m x n x 2k product per modulus) instead of the Karatsuba sub-products; slices, residue
-    planes and C against the oracle, fast and accurate, all three compute types, ops N/T/C"""
+def test_complex_karatsuba_products_forced():
+    """GEMMUL8_CPLX_PRODUCTS=karatsuba (child process): complex products as Karatsuba sub-products
+    at shapes where the size rule keeps the big matrix; Karatsuba slices, the three residue
+    sub-planes and C against the oracle, fast and accurate (big-matrix bound), all three compute
+    types, ops N/T/C, N = 20, f32 operands, low-memory mode and chunked k"""
     import subprocess
     code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
             "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
             "import gemmul8 as G\n"
             "rng = np.random.default_rng(11)\n"
             "L = G.layout(70, 90, 333, 9, G.COMPLEX_BIG_MATRIX_ENCODE)\n"
-            "assert L['nsub'] == 1, L\n"
+            "assert L['nsub'] == 3, L\n"
             "for ct in (1, 2, 3):\n"
             "    check_full(randmat_np(rng, 70, 333, dtype=np.complex128), randmat_np(rng, 333, 90, dtype=np.complex128), 12, ctype=ct)\n"
             "    check_full(randmat_np(rng, 41, 62, dtype=np.complex128), randmat_np(rng, 62, 35, dtype=np.complex128), 12, fast=False, ctype=ct)\n"
             "check_full(randmat_np(rng, 50, 33, dtype=np.complex64), randmat_np(rng, 40, 50, dtype=np.complex64), 7, opA=2, opB=1)\n"
+            "check_full(randmat_np(rng, 33, 50, dtype=np.complex128), randmat_np(rng, 40, 50, dtype=np.complex128), 12, opB=2)\n"
+            "check_full(randmat_np(rng, 30, 47, dtype=np.complex64), randmat_np(rng, 47, 30, dtype=np.complex64), 7, fast=False, opA=2, opB=0)\n"
+            "check_full(randmat_np(rng, 300, 260, dtype=np.complex128), randmat_np(rng, 260, 513, dtype=np.complex128), 20)\n"
+            "check_full(randmat_np(rng, 40, 50, dtype=np.complex64), randmat_np(rng, 50, 30, dtype=np.complex128), 9, out_dtype=np.complex128)\n"
+            "check_full(randmat_np(rng, 45, 70, dtype=np.complex64), randmat_np(rng, 70, 38, dtype=np.complex64), 16)\n"
+            "check_full(randmat_np(rng, 5, 70000, dtype=np.complex128), randmat_np(rng, 70000, 6, dtype=np.complex128), 12)\n"
+            "import torch\n"
+            "m, n, k, N = 300, 260, 513, 14\n"
+            "A = torch.randn((k, m), dtype=torch.complex128, device='cuda'); B = torch.randn((n, k), dtype=torch.complex128, device='cuda')\n"
+            "Cs = []\n"
+            "for S in (None, 2, 5):\n"
+            "    W = G.alloc_work(m, n, k, N, 1, slice_planes=S); C = torch.empty((n, m), dtype=torch.complex128, device='cuda')\n"
+            "    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, True, W, 1, slice_planes=S); Cs.append(C.cpu())\n"
+            "assert all(torch.equal(Cs[0].view(torch.float64), c.view(torch.float64)) for c in Cs[1:])\n"
             "print('OK')")
     tdir = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(tdir)
-    env = dict(os.environ, GEMMUL8_CPLX_BIGMATRIX="1")
+    env = dict(os.environ, GEMMUL8_CPLX_PRODUCTS="karatsuba")
     r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]

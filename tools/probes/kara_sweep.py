@@ -1,6 +1,6 @@
-"""Complex GEMM time, Karatsuba sub-products vs the big-matrix product (GEMMUL8_CPLX_BIGMATRIX=1 in a
-child process), over square and skinny shapes, fast mode N = 12: picks the size rule in
-csrc/oz2_common.hpp make_layout.  Usage: python tools/probes/kara_sweep.py [out.json]"""
+"""Complex GEMM time, Karatsuba sub-products vs the big-matrix product (GEMMUL8_CPLX_PRODUCTS forced
+in a child process each), over square and skinny shapes, fast mode N = 12: the measurements behind
+the size rule of csrc/oz2_common.hpp kara_default.  Usage: python tools/probes/kara_sweep.py [out.json]"""
 import json
 import os
 import subprocess
@@ -46,7 +46,7 @@ if __name__ == "__main__":
         child()
         sys.exit(0)
     res = {}
-    for tag, env in (("kara", {}), ("bigmatrix", {"GEMMUL8_CPLX_BIGMATRIX": "1"})):
+    for tag, env in (("kara", {"GEMMUL8_CPLX_PRODUCTS": "karatsuba"}), ("bigmatrix", {"GEMMUL8_CPLX_PRODUCTS": "bigmatrix"})):
         r = subprocess.run([sys.executable, __file__, "--child"], env=dict(os.environ, **env), capture_output=True,
                            text=True, timeout=300)
         if r.returncode != 0:
