@@ -145,24 +145,38 @@ template <> struct BlasEpi<3> {
     }
 };
 
-// Karatsuba complex: the residues of Re = P1 - P2 and Im = P3 - P1 - P2 modulo p_i, for the 8
-// bytes of one load of each sub-plane (byte e of each word); the moduli are compile-time constants.
+// Karatsuba complex: the residues of Re = P1 - P2 and Im = P3 - P1 - P2 modulo p, for 8 bytes at once.
+// Bytes go to 16-bit lanes (even / odd bytes of each dword); in a lane d = b1 - b2 wraps mod 2^16 when
+// negative, so (d, d + p) holds exactly one value below p, the residue; likewise (q, q + p, q + 2p) for
+// q = b3 - b1 - b2 in (-2p, p).  Packed u16 add / sub / min (v_pk_*_u16): about 6 ops per byte pair.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+template <int P>
+__device__ __forceinline__ void kara_dword(uint32_t x1, uint32_t x2, uint32_t x3, uint32_t &re, uint32_t &im) {
+    const u16x2 p1 = {(unsigned short)P, (unsigned short)P}, p2 = {(unsigned short)(2 * P), (unsigned short)(2 * P)};
+    auto lanes = [&](uint32_t a1, uint32_t a2, uint32_t a3, uint32_t &r, uint32_t &t) {
+        const u16x2 e1 = __builtin_bit_cast(u16x2, a1), e2 = __builtin_bit_cast(u16x2, a2), e3 = __builtin_bit_cast(u16x2, a3);
+        const u16x2 d = e1 - e2;
+        r = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(d, d + p1));
+        const u16x2 q = e3 - (e1 + e2);
+        t = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_elementwise_min(q, q + p1), q + p2));
+    };
+    constexpr uint32_t LO = 0x00ff00ffu;
+    uint32_t rE, tE, rO, tO;
+    lanes(x1 & LO, x2 & LO, x3 & LO, rE, tE);
+    lanes((x1 >> 8) & LO, (x2 >> 8) & LO, (x3 >> 8) & LO, rO, tO);
+    re = rE | (rO << 8);
+    im = tE | (tO << 8);
+}
 template <unsigned N, unsigned... I>
-__device__ __forceinline__ void kara_residues(const uint64_t (&w1)[N], const uint64_t (&w2)[N], const uint64_t (&w3)[N],
-                                              int e, uint8_t (&re)[N], uint8_t (&im)[N],
-                                              std::integer_sequence<unsigned, I...>) {
+__device__ __forceinline__ void kara_words(const uint64_t (&w1)[N], const uint64_t (&w2)[N], const uint64_t (&w3)[N],
+                                           uint64_t (&re)[N], uint64_t (&im)[N], std::integer_sequence<unsigned, I...>) {
     auto one = [&](auto ic) {
         constexpr unsigned i = decltype(ic)::value;
-        constexpr int p = oz2_p[i];
-        const int b1 = (int)((w1[i] >> (8 * e)) & 0xff), b2 = (int)((w2[i] >> (8 * e)) & 0xff);
-        const int b3 = (int)((w3[i] >> (8 * e)) & 0xff);
-        int r = b1 - b2;
-        r += r < 0 ? p : 0;
-        int t = b3 - b1 - b2;
-        t += t < 0 ? p : 0;
-        t += t < 0 ? p : 0;
-        re[i] = (uint8_t)r;
-        im[i] = (uint8_t)t;
+        uint32_t r0, i0, r1, i1;
+        kara_dword<oz2_p[i]>((uint32_t)w1[i], (uint32_t)w2[i], (uint32_t)w3[i], r0, i0);
+        kara_dword<oz2_p[i]>((uint32_t)(w1[i] >> 32), (uint32_t)(w2[i] >> 32), (uint32_t)(w3[i] >> 32), r1, i1);
+        re[i] = (uint64_t)r0 | ((uint64_t)r1 << 32);
+        im[i] = (uint64_t)i0 | ((uint64_t)i1 << 32);
     };
     (one(std::integral_constant<unsigned, I>{}), ...);
 }
@@ -191,29 +205,19 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     E *wb = buf[wv];
     for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
         const int sB = a.sftB[col];
-        if constexpr (KARA) {
-          if (nr > 0) {
-            uint64_t w1[N], w2[N], w3[N];
-            const size_t off = col * a.ldr + r0;
-            load_rows<N>(a, off, nr == CRT_ROWS, nr, w1);
-            load_rows<N>(a, off + a.sub, nr == CRT_ROWS, nr, w2);
-            load_rows<N>(a, off + 2 * a.sub, nr == CRT_ROWS, nr, w3);
-#pragma unroll
-            for (int e = 0; e < CRT_ROWS; ++e) {
-                uint8_t rr[N], ri[N];
-                kara_residues<N>(w1, w2, w3, e, rr, ri, std::make_integer_sequence<unsigned, N>{});
-                const int sft = (int)sa[e] + sB;
-                const double vr = scalbn(crt_value_const<N, NUMM1>(rr, std::make_integer_sequence<unsigned, N>{}), sft);
-                const double vi = scalbn(crt_value_const<N, NUMM1>(ri, std::make_integer_sequence<unsigned, N>{}), sft);
-                if constexpr (OT == 2) wb[lane * CRT_ROWS + e] = make_double2(vr, vi);
-                else if constexpr (OT == 3) wb[lane * CRT_ROWS + e] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
-            }
-          }
-        } else if (nr > 0) {
+        if (nr > 0) {
             uint64_t w[N], wi[N];
             const size_t off = col * a.ldr + r0;
-            load_rows<N>(a, off, nr == CRT_ROWS, nr, w);
-            if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == CRT_ROWS && (a.imag_off & 7) == 0, nr, wi);
+            if constexpr (KARA) {
+                uint64_t w1[N], w2[N], w3[N];
+                load_rows<N>(a, off, nr == CRT_ROWS, nr, w1);
+                load_rows<N>(a, off + a.sub, nr == CRT_ROWS, nr, w2);
+                load_rows<N>(a, off + 2 * a.sub, nr == CRT_ROWS, nr, w3);
+                kara_words<N>(w1, w2, w3, w, wi, std::make_integer_sequence<unsigned, N>{});
+            } else {
+                load_rows<N>(a, off, nr == CRT_ROWS, nr, w);
+                if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == CRT_ROWS && (a.imag_off & 7) == 0, nr, wi);
+            }
 #pragma unroll
             for (int e = 0; e < CRT_ROWS; ++e) {
                 uint8_t r[N];
