@@ -26,6 +26,11 @@ void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool acc
 void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
                   size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st,
                   bool btail_quirk = false);
+// mode 0 slices of both real operands of one precision in a single launch (false: not applicable,
+// nothing launched)
+bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
+                       const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
+                       const ModParams &MP, hipStream_t st);
 // cplx_rows: complex A bound of row v = max(bound[v], bound[v + nvec]) (scaling.hpp:2561-2588)
 void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
                              hipStream_t st, bool cplx_rows = false);

@@ -297,12 +297,13 @@ __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict_
 // stores the last k mod 4 imaginary magnitudes outside the column, leaving them 0 in
 // the bound product -- extract_B8i_kernel_bigmatrix, scaling.hpp:2313-2321).
 // ------------------------------------------------------------------
+template <typename R, bool CPLX> using EncTile = R[CPLX ? 32 : 64][64 + 1][CPLX ? 2 : 1];
+
 template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
-__global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__restrict__ X, size_t ld, size_t nvec,
-                                                                   size_t len, const int16_t *__restrict__ sft,
-                                                                   int8_t *__restrict__ out, size_t plane,
-                                                                   size_t ksteps, size_t kblk, size_t vmax,
-                                                                   int flags, ModParams MP, ModGroups G) {
+__device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                            const int16_t *__restrict__ sft, int8_t *__restrict__ out, size_t plane,
+                                            size_t ksteps, size_t kblk, size_t vmax, int flags, const ModParams &MP,
+                                            const ModGroups &G, unsigned bx, unsigned by, EncTile<R, CPLX> &tile) {
     constexpr int KT = CPLX ? 32 : 64;
     constexpr int NT = CPLX ? 128 : 256;
     constexpr int NC = CPLX ? 2 : 1;
@@ -310,10 +311,9 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
     // pieces of the same vectors (walking the vectors instead puts every co-running block at
     // the same offset modulo the vector stride, i.e. on the same HBM channels)
     const bool kfirst = CONTIG && (flags & ENC_KFIRST);
-    const size_t v0 = (size_t)(kfirst ? blockIdx.y : blockIdx.x) * 64;
-    const size_t e0 = (size_t)(kfirst ? blockIdx.x : blockIdx.y) * KT;
+    const size_t v0 = (size_t)(kfirst ? by : bx) * 64;
+    const size_t e0 = (size_t)(kfirst ? bx : by) * KT;
     const int tid = threadIdx.x;
-    __shared__ R tile[KT][64 + 1][NC];
 
     // stage the tile, coalesced along whichever index is contiguous in HBM; interior tiles
     // load without per-element guards so all loads are in flight at once
@@ -627,6 +627,44 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
     }
 }
 
+template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
+__global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__restrict__ X, size_t ld, size_t nvec,
+                                                                   size_t len, const int16_t *__restrict__ sft,
+                                                                   int8_t *__restrict__ out, size_t plane,
+                                                                   size_t ksteps, size_t kblk, size_t vmax,
+                                                                   int flags, ModParams MP, ModGroups G) {
+    __shared__ EncTile<R, CPLX> tile;
+    encode_body<R, CPLX, CONTIG, IS_A, MODE>(X, ld, nvec, len, sft, out, plane, ksteps, kblk, vmax, flags, MP, G,
+                                             blockIdx.x, blockIdx.y, tile);
+}
+
+// Both operands' slices in one launch (small problems, one stream): blocks [0, gx*gy of A) encode A,
+// the rest B.  Saves a launch boundary and lets A's and B's tiles share the chip.
+struct EncOperand {
+    const void *X;
+    size_t ld, nvec, len;
+    const int16_t *sft;
+    int8_t *out;
+    size_t plane, vmax;
+    int flags;
+    unsigned gx, gy;
+};
+template <typename R, bool CPLX, bool CONTIG_A, bool CONTIG_B>
+__global__ __launch_bounds__(CPLX ? 128 : 256) void encode_pair_kernel(EncOperand a, EncOperand b, size_t ksteps,
+                                                                        size_t kblk, ModParams MP, ModGroups G) {
+    __shared__ EncTile<R, CPLX> tile;
+    const unsigned na = a.gx * a.gy;
+    if (blockIdx.x < na) {
+        encode_body<R, CPLX, CONTIG_A, true, 0>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.sft, a.out, a.plane,
+                                                ksteps, kblk, a.vmax, a.flags, MP, G, blockIdx.x % a.gx, blockIdx.x / a.gx,
+                                                tile);
+    } else {
+        const unsigned t = blockIdx.x - na;
+        encode_body<R, CPLX, CONTIG_B, false, 0>(static_cast<const R *>(b.X), b.ld, b.nvec, b.len, b.sft, b.out, b.plane,
+                                                 ksteps, kblk, b.vmax, b.flags, MP, G, t % b.gx, t / b.gx, tile);
+    }
+}
+
 // accurate mode: sft = sft0 + floor_rd(-0.51*log2(amax) + log2M)  (int8tc::compute_sft, scaling.hpp:1504-1506)
 __global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, const int32_t *__restrict__ bound,
                                              size_t nvec, float log2M, int16_t *__restrict__ sft_out, int cplx_rows) {
@@ -730,6 +768,48 @@ void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, cons
         else OZ2_LE(float, false, false);
     }
 #undef OZ2_LE
+}
+
+template <typename R, bool CA, bool CB>
+static void launch_encode_pair(const EncOperand &a, const EncOperand &b, const Layout &L, const ModParams &MP,
+                               hipStream_t st) {
+    const ModGroups G = make_groups(MP, L.N);
+    encode_pair_kernel<R, false, CA, CB><<<dim3(a.gx * a.gy + b.gx * b.gy), dim3(256), 0, st>>>(a, b, L.ksteps, L.kblk,
+                                                                                                MP, G);
+}
+
+bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
+                       const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
+                       const ModParams &MP, hipStream_t st) {
+    // real operands of one precision (the same ModGroups and tile type); anything else: two launches
+    if (dA.cplx || dB.cplx || dA.dbl != dB.dbl || L.kblk == 0) return false;
+    constexpr int KT = 64;
+    auto operand = [&](const OperandDesc &d, size_t nvec, const int16_t *sft, int8_t *out, size_t plane, size_t vpad) {
+        EncOperand e{};
+        e.X = d.ptr;
+        e.ld = d.ld;
+        e.nvec = nvec;
+        e.len = len;
+        e.sft = sft;
+        e.out = out;
+        e.plane = plane;
+        e.vmax = vpad;
+        e.flags = d.contig ? ENC_KFIRST : 0;  // (as launch_encode: k-first block order for contiguous vectors)
+        vpad = round_up(vpad, 64);
+        e.gx = d.contig ? (unsigned)(L.kblk / KT) : (unsigned)(vpad / 64);
+        e.gy = d.contig ? (unsigned)(vpad / 64) : (unsigned)(L.kblk / KT);
+        return e;
+    };
+    const EncOperand a = operand(dA, m, sftA, outA, L.planeA, L.m_pad);
+    const EncOperand b = operand(dB, n, sftB, outB, L.planeB, L.n_pad);
+    if (dA.dbl) {
+        if (dA.contig) { if (dB.contig) launch_encode_pair<double, true, true>(a, b, L, MP, st); else launch_encode_pair<double, true, false>(a, b, L, MP, st); }
+        else { if (dB.contig) launch_encode_pair<double, false, true>(a, b, L, MP, st); else launch_encode_pair<double, false, false>(a, b, L, MP, st); }
+    } else {
+        if (dA.contig) { if (dB.contig) launch_encode_pair<float, true, true>(a, b, L, MP, st); else launch_encode_pair<float, true, false>(a, b, L, MP, st); }
+        else { if (dB.contig) launch_encode_pair<float, false, true>(a, b, L, MP, st); else launch_encode_pair<float, false, false>(a, b, L, MP, st); }
+    }
+    return true;
 }
 
 void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
