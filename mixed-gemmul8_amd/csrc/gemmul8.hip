@@ -257,9 +257,13 @@ static void operand_encode(const Call &c, const Views &v, bool is_A, unsigned j0
 static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1, bool bound_ready) {
     if (!c.fast && !bound_ready) phase_bound(c, v);
     if (!c.lane) {
-        // one stream (small problems): both shift passes, then both operands' slices in one launch
-        operand_shifts(c, v, true, c.st);
-        operand_shifts(c, v, false, c.st);
+        // one stream (small problems): both operands' shifts, then both operands' slices, one launch each
+        // where the operand forms allow it
+        if (!(c.fast && split_stats_pair(c.A, c.m, c.B, c.n, c.k, c.VT, oz2_log2M_fast[c.N - 2], v.sftA, v.sftB,
+                                         c.st))) {
+            operand_shifts(c, v, true, c.st);
+            operand_shifts(c, v, false, c.st);
+        }
         const Layout &L = v.L;
         if (split_encode_pair(c.A, c.m, c.B, c.n, c.k, v.sftA, v.sftB, v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB, L,
                               sub_mod_params(c.N, j0, j1), c.st))

@@ -26,6 +26,10 @@ void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool acc
 void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
                   size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st,
                   bool btail_quirk = false);
+// fast-mode shifts of A (real f64 rows, strided) and B (real f64 columns, contiguous) in one launch
+// (false: not applicable, nothing launched)
+bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
+                      float log2M, int16_t *sftA, int16_t *sftB, hipStream_t st);
 // mode 0 slices of both real operands of one precision in a single launch (false: not applicable,
 // nothing launched)
 bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,

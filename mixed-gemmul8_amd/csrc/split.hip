@@ -151,12 +151,15 @@ __device__ __forceinline__ void accum(R re, R im, R &amax, R &sum) {
 // ------------------------------------------------------------------
 // pass 1a: contiguous vectors (B op N, A op T): one vector per VT-thread block
 // ------------------------------------------------------------------
+// vector v by the VT threads t = 0..VT-1 of a block (or of one half of a 2 VT block: every thread of
+// the block must call it, it holds a barrier); v >= nvec computes nothing and stores nothing
 template <typename R, bool CPLX, int VT, bool ACCU>
-__global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
-                                                         float log2M, int16_t *__restrict__ sft_out) {
-    const size_t v = blockIdx.x;
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const R *__restrict__ x = X + (CPLX ? 2 : 1) * v * ld;
+__device__ __forceinline__ void stats_contig_body(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
+                                                  float log2M, int16_t *__restrict__ sft_out, size_t v, int t,
+                                                  R (&grp)[32], R (&gmax)[8]) {
+    const int lane = t & 63, w = t >> 6;
+    const R *__restrict__ x = X + (CPLX ? 2 : 1) * (v < nvec ? v : 0) * ld;
+    if (v >= nvec) len = 0;
     R amax = 0, sum = 0;
     // loads are issued in unguarded batches of U ahead of the round-up chain (whose
     // mode-register writes would otherwise serialise each load behind the previous fma)
@@ -174,8 +177,6 @@ __global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ 
         load_elem<R, CPLX>(x, e, re, im);
         accum<R, CPLX>(re, im, amax, sum);
     }
-    __shared__ R grp[32];
-    __shared__ R gmax[8];
     amax = wave_max<R>(amax);
     if (!ACCU) {
         sum = ref_wave_sum<R>(sum);
@@ -188,14 +189,22 @@ __global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ 
         R mx = lane < VT / 64 ? gmax[lane] : R(0);
         mx = wave_max<R>(mx);
         if (ACCU) {
-            if (lane == 0) sft_out[v] = (int16_t)(5 - (std::is_same<R, double>::value ? ilogb((double)mx) : ilogbf((float)mx)));
+            if (lane == 0 && v < nvec)
+                sft_out[v] = (int16_t)(5 - (std::is_same<R, double>::value ? ilogb((double)mx) : ilogbf((float)mx)));
         } else {
             R s2 = (lane >= 32 && lane - 32 < VT / 32) ? grp[lane - 32] : R(0);
             s2 = ref_wave_sum<R>(s2);
             const R nrm = __shfl(s2, 32);
-            if (lane == 0) sft_out[v] = (int16_t)(-compute_sft(mx, nrm, log2M));
+            if (lane == 0 && v < nvec) sft_out[v] = (int16_t)(-compute_sft(mx, nrm, log2M));
         }
     }
+}
+template <typename R, bool CPLX, int VT, bool ACCU>
+__global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
+                                                         float log2M, int16_t *__restrict__ sft_out) {
+    __shared__ R grp[32];
+    __shared__ R gmax[8];
+    stats_contig_body<R, CPLX, VT, ACCU>(X, ld, len, nvec, log2M, sft_out, blockIdx.x, threadIdx.x, grp, gmax);
 }
 
 // ------------------------------------------------------------------
@@ -207,15 +216,22 @@ __global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ 
 // ROWS = 16 for m >= 4096; 8 / 4 below, where m/16 blocks leave CUs idle (1024: 15.2 -> 9.6 us,
 // 2048: 23.2 -> 17.3 us; narrower rows cost HBM efficiency at 4096 and up, tools/probes/run_stats_rows.sh).
 // ------------------------------------------------------------------
+template <typename R, int VT, int ROWS> struct StridedShared {
+    R part[ROWS][VT + 1];
+    R pmax[ROWS][256 / ROWS + 1];
+};
 template <typename R, bool CPLX, int VT, bool ACCU, int ROWS>
-__global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
-                                                           float log2M, int16_t *__restrict__ sft_out) {
+__device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
+                                                   float log2M, int16_t *__restrict__ sft_out, unsigned bx,
+                                                   StridedShared<R, VT, ROWS> &sh) {
     constexpr int SLOTS = 256 / ROWS;
     constexpr int NA = VT / SLOTS;
     constexpr int U = (ROWS == 16 || NA >= 16) ? 1 : 16 / NA;  // batching measured slower at 16 rows
     static_assert(SLOTS <= 64 && NA >= 1, "one reduction lane per slot");
+    auto &part = sh.part;
+    auto &pmax = sh.pmax;
     const int tid = threadIdx.x, row = tid % ROWS, slot = tid / ROWS;
-    const size_t v = (size_t)blockIdx.x * ROWS + row;
+    const size_t v = (size_t)bx * ROWS + row;
     R acc[NA];
 #pragma unroll
     for (int c = 0; c < NA; ++c) acc[c] = 0;
@@ -253,8 +269,6 @@ __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict_
             }
         }
     }
-    __shared__ R part[ROWS][VT + 1];
-    __shared__ R pmax[ROWS][SLOTS + 1];
     if (!ACCU) {
 #pragma unroll
         for (int c = 0; c < NA; ++c) part[row][slot + SLOTS * c] = acc[c];
@@ -264,7 +278,7 @@ __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict_
     const int w = tid >> 6, lane = tid & 63;
 #pragma unroll 1
     for (int r2 = w; r2 < ROWS; r2 += 4) {
-        const size_t v2 = (size_t)blockIdx.x * ROWS + r2;
+        const size_t v2 = (size_t)bx * ROWS + r2;
         R mx = lane < SLOTS ? pmax[r2][lane] : R(0);
         mx = wave_max<R>(mx);
         if (ACCU) {
@@ -283,6 +297,33 @@ __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict_
         gv = ref_wave_sum<R>(gv);
         const R nrm = __shfl(gv, 32);
         if (lane == 0 && v2 < nvec) sft_out[v2] = (int16_t)(-compute_sft(mx, nrm, log2M));
+    }
+}
+template <typename R, bool CPLX, int VT, bool ACCU, int ROWS>
+__global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
+                                                           float log2M, int16_t *__restrict__ sft_out) {
+    __shared__ StridedShared<R, VT, ROWS> sh;
+    stats_strided_body<R, CPLX, VT, ACCU, ROWS>(X, ld, len, nvec, log2M, sft_out, blockIdx.x, sh);
+}
+
+// Both operands' fast-mode shifts in one launch (small problems, one stream; real f64, A rows strided,
+// B columns contiguous, VT = 128): blocks [0, ga) sweep ROWS rows of A each, the others two columns of
+// B each (one per 128-thread half, the contiguous pass's own block shape).
+template <int ROWS>
+__global__ __launch_bounds__(256) void stats_pair_kernel(const double *__restrict__ A, size_t lda, size_t m,
+                                                        const double *__restrict__ B, size_t ldb, size_t n, size_t len,
+                                                        float log2M, int16_t *__restrict__ sftA,
+                                                        int16_t *__restrict__ sftB, unsigned ga) {
+    __shared__ StridedShared<double, 128, ROWS> sh;
+    __shared__ double grp[2][32];
+    __shared__ double gmax[2][8];
+    if (blockIdx.x < ga) {
+        stats_strided_body<double, false, 128, false, ROWS>(A, lda, len, m, log2M, sftA, blockIdx.x, sh);
+    } else {
+        const int half = threadIdx.x >> 7;
+        const size_t v = 2 * (size_t)(blockIdx.x - ga) + half;
+        stats_contig_body<double, false, 128, false>(B, ldb, len, n, log2M, sftB, v, threadIdx.x & 127, grp[half],
+                                                     gmax[half]);
     }
 }
 
@@ -690,6 +731,17 @@ void zero_i32(int32_t *p, size_t n, hipStream_t st) {
 // ------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------
+// rows per block of the strided pass: enough blocks to give every CU several (m/16 < 2 per CU leaves
+// the chip latency-bound); GEMMUL8_STATS_ROWS overrides (probe / A-B runs)
+static int stats_rows(size_t nvec) {
+    static const int forced = [] {
+        const char *e = getenv("GEMMUL8_STATS_ROWS");
+        const int r = e ? atoi(e) : 0;
+        return (r == 4 || r == 8 || r == 16) ? r : 0;
+    }();
+    return forced ? forced : nvec >= 4096 ? 16 : nvec >= 2048 ? 8 : 4;
+}
+
 template <typename R, bool CPLX>
 static void launch_stats(const void *X, size_t ld, bool contig, size_t len, size_t nvec, int VT, bool accurate,
                          float log2M, int16_t *out, hipStream_t st) {
@@ -700,14 +752,7 @@ static void launch_stats(const void *X, size_t ld, bool contig, size_t len, size
         else { if (accurate) OZ2_SC(128, true); else OZ2_SC(128, false); }
 #undef OZ2_SC
     } else {
-        // rows per block: enough blocks to give every CU several (m/16 < 2 per CU leaves the
-        // chip latency-bound); GEMMUL8_STATS_ROWS overrides (probe / A-B runs)
-        static const int forced = [] {
-            const char *e = getenv("GEMMUL8_STATS_ROWS");
-            const int r = e ? atoi(e) : 0;
-            return (r == 4 || r == 8 || r == 16) ? r : 0;
-        }();
-        const int rows = forced ? forced : nvec >= 4096 ? 16 : nvec >= 2048 ? 8 : 4;
+        const int rows = stats_rows(nvec);
         const unsigned g = (unsigned)((nvec + rows - 1) / rows);
 #define OZ2_SS(vt, ac, rw) stats_strided_kernel<R, CPLX, vt, ac, rw><<<dim3(g), dim3(256), 0, st>>>(x, ld, len, nvec, log2M, out)
 #define OZ2_SSR(vt, ac) do { if (rows == 16) OZ2_SS(vt, ac, 16); else if (rows == 8) OZ2_SS(vt, ac, 8); else OZ2_SS(vt, ac, 4); } while (0)
@@ -768,6 +813,20 @@ void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, cons
         else OZ2_LE(float, false, false);
     }
 #undef OZ2_LE
+}
+
+bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
+                      float log2M, int16_t *sftA, int16_t *sftB, hipStream_t st) {
+    if (dA.cplx || dB.cplx || !dA.dbl || !dB.dbl || dA.contig || !dB.contig || VT != 128) return false;
+    const int rows = stats_rows(m);
+    const unsigned ga = (unsigned)((m + rows - 1) / rows), gb = (unsigned)((n + 1) / 2);
+    const double *a = static_cast<const double *>(dA.ptr), *b = static_cast<const double *>(dB.ptr);
+#define OZ2_SP(r) stats_pair_kernel<r><<<dim3(ga + gb), dim3(256), 0, st>>>(a, dA.ld, m, b, dB.ld, n, len, log2M, sftA, sftB, ga)
+    if (rows == 16) OZ2_SP(16);
+    else if (rows == 8) OZ2_SP(8);
+    else OZ2_SP(4);
+#undef OZ2_SP
+    return true;
 }
 
 template <typename R, bool CA, bool CB>
