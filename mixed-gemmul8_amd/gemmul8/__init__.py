@@ -74,12 +74,25 @@ def _check(rc):
         raise Gemmul8Error(f"gemmul8 error {rc}: {_ERR.get(rc, 'unknown')}")
 
 
+class _HostScalar:
+    """host alpha/beta buffer of the output type (a ctypes object: a numpy array costs ~3 us per call)"""
+    __slots__ = ("buf", "ptr")
+
+    def __init__(self, x, dtype):
+        if dtype in (torch.complex128, torch.complex64):
+            x = complex(x)
+            self.buf = ((ctypes.c_double if dtype == torch.complex128 else ctypes.c_float) * 2)(x.real, x.imag)
+        elif dtype == torch.float64:
+            self.buf = ctypes.c_double(x)
+        elif dtype == torch.float32:
+            self.buf = ctypes.c_float(x)
+        else:
+            raise KeyError(dtype)
+        self.ptr = ctypes.addressof(self.buf)
+
+
 def _scalar(x, dtype):
-    """host alpha/beta buffer of the output type"""
-    import numpy as np
-    npt = {torch.float64: np.float64, torch.float32: np.float32, torch.complex128: np.complex128,
-           torch.complex64: np.complex64}[dtype]
-    return np.array([x], dtype=npt)
+    return _HostScalar(x, dtype)
 
 
 def workSize(m, n, k, num_moduli, computeType=REAL_DEFAULT, slice_planes=None):
@@ -109,12 +122,12 @@ def gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fas
     al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
     pt = (ctypes.c_double * 4)() if phase_times else None
     if slice_planes:
-        rc = lib.gemmul8_gemm_lowmem(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ctypes.data, A.data_ptr(),
-                                     lda, B.data_ptr(), ldb, be.ctypes.data, C.data_ptr(), ldc, num_moduli,
+        rc = lib.gemmul8_gemm_lowmem(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ptr, A.data_ptr(),
+                                     lda, B.data_ptr(), ldb, be.ptr, C.data_ptr(), ldc, num_moduli,
                                      int(bool(fastmode)), work.data_ptr(), computeType, slice_planes, pt)
     else:
-        rc = lib.gemmul8_gemm(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ctypes.data, A.data_ptr(), lda,
-                              B.data_ptr(), ldb, be.ctypes.data, C.data_ptr(), ldc, num_moduli, int(bool(fastmode)),
+        rc = lib.gemmul8_gemm(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ptr, A.data_ptr(), lda,
+                              B.data_ptr(), ldb, be.ptr, C.data_ptr(), ldc, num_moduli, int(bool(fastmode)),
                               work.data_ptr(), computeType, pt)
     _check(rc)
     return list(pt) if phase_times else None
@@ -156,8 +169,8 @@ def products(m, n, k, num_moduli, work, mod_begin=0, mod_end=None, computeType=R
 def recombine(m, n, k, num_moduli, alpha, beta, C, ldc, work, computeType=REAL_DEFAULT, stream=None):
     """CRT of all residue planes in `work` + scaling + alpha/beta epilogue into C."""
     al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
-    _check(lib.gemmul8_recombine(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], computeType, al.ctypes.data,
-                                 be.ctypes.data, C.data_ptr(), ldc, work.data_ptr()))
+    _check(lib.gemmul8_recombine(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], computeType, al.ptr,
+                                 be.ptr, C.data_ptr(), ldc, work.data_ptr()))
 
 
 def residue_planes(work, m, n, k, num_moduli, mod_begin=0, mod_end=None, computeType=REAL_DEFAULT):
