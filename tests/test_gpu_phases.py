@@ -65,6 +65,35 @@ def test_moduli_ranges_compose(m, n, k, N, fast, dt):
     assert _same(Ct.t(), ref)
 
 
+@pytest.mark.parametrize("fast", [True, False])
+def test_moduli_ranges_compose_complex_karatsuba(fast):
+    """complex at a shape where the size rule runs Karatsuba sub-products (k >= 3072, m >= 1024): split /
+    products over moduli ranges + recombine == one call, and the residue planes hold 3 sub-planes"""
+    import torch
+    import gemmul8 as G
+    m, n, k, N = 1024, 300, 3100, 12
+    ct = G.COMPLEX_BIG_MATRIX_ENCODE
+    L = G.layout(m, n, k, N, ct)
+    if L["nsub"] != 3:
+        pytest.skip("GEMMUL8_CPLX_PRODUCTS forces the big matrix")
+    g = torch.Generator(device="cuda").manual_seed(3)
+    A = torch.randn((k, m), dtype=torch.complex128, device="cuda", generator=g)  # column-major m x k
+    B = torch.randn((n, k), dtype=torch.complex128, device="cuda", generator=g)  # column-major k x n
+    ref = torch.empty((n, m), dtype=torch.complex128, device="cuda")
+    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, ref, m, N, fast, G.alloc_work(m, n, k, N, ct), ct)
+    work = G.alloc_work(m, n, k, N, ct)
+    if not fast:
+        G.split_bound(0, 0, m, n, k, A, m, B, k, N, work, torch.complex128, ct)
+    for j0, j1 in ((0, 1), (1, N // 2), (N // 2, N)):
+        G.split(0, 0, m, n, k, A, m, B, k, N, fast, work, torch.complex128, j0, j1, ct, bound_ready=not fast)
+        G.products(m, n, k, N, work, j0, j1, ct)
+    Ct = torch.empty((n, m), dtype=torch.complex128, device="cuda")
+    G.recombine(m, n, k, N, 1.0, 0.0, Ct, m, work, ct)
+    torch.cuda.synchronize()
+    assert _same(Ct, ref)
+    assert G.residue_planes(work, m, n, k, N, 0, N, ct).shape == (N, 3 * L["vsA"] * L["vsB"])
+
+
 def test_accurate_row_blocks_with_combined_bound():
     import torch
     from gemmul8 import dist as GD
