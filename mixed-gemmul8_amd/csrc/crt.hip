@@ -12,7 +12,8 @@
 // template parameter (19 instantiations) so every plane load is unguarded and
 // the accumulation fully unrolled; the weights are compile-time constants of the
 // instantiation (the reference uploads them to __constant__ on every call,
-// gemmul8.cu:236-241).
+// gemmul8.cu:236-241).  Complex outputs read the real and imaginary residues from rows r and
+// r + m of the big-matrix planes, or combine them from the three Karatsuba sub-planes (KARA).
 #include <utility>
 
 #include "oz2_split.hpp"

@@ -2,7 +2,8 @@
 //
 // Replaces the reference's per-modulus hipblasGemmEx + conv_32i_2_8u pair
 // (GEMMul8/src/gemmul8.cu:259-275, conv_32i_2_8u.hpp:7-71): one launch covers all
-// N moduli (grid.y = modulus), each 256x256 output tile accumulates with
+// N moduli (grid.y = modulus; 3 j + s for the Karatsuba complex sub-products s = 0..2 of
+// modulus j, an instantiation of its own), each 256x256 output tile accumulates with
 // v_mfma_i32_16x16x64_i8 and is reduced mod p_i in the epilogue, so the int32
 // product never reaches HBM (the reference writes and re-reads 4*m*n bytes per
 // modulus).  The accurate-mode bound product (scaling.hpp:3113-3121) runs the same
