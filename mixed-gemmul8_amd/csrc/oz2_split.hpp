@@ -30,7 +30,7 @@ void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, cons
 // (false: not applicable, nothing launched)
 bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
                       float log2M, int16_t *sftA, int16_t *sftB, hipStream_t st);
-// mode 0 slices of both real operands of one precision in a single launch (false: not applicable,
+// mode 0 slices of both operands (one element type) in a single launch (false: not applicable,
 // nothing launched)
 bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
                        const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,

@@ -829,21 +829,29 @@ bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, si
     return true;
 }
 
-template <typename R, bool CA, bool CB>
+template <typename R, bool CPLX, bool CA, bool CB>
 static void launch_encode_pair(const EncOperand &a, const EncOperand &b, const Layout &L, const ModParams &MP,
                                hipStream_t st) {
     const ModGroups G = make_groups(MP, L.N);
-    encode_pair_kernel<R, false, CA, CB><<<dim3(a.gx * a.gy + b.gx * b.gy), dim3(256), 0, st>>>(a, b, L.ksteps, L.kblk,
-                                                                                                MP, G);
+    encode_pair_kernel<R, CPLX, CA, CB><<<dim3(a.gx * a.gy + b.gx * b.gy), dim3(CPLX ? 128 : 256), 0, st>>>(
+        a, b, L.ksteps, L.kblk, MP, G);
+}
+template <typename R, bool CPLX>
+static void launch_encode_pair_ops(bool ca, bool cb, const EncOperand &a, const EncOperand &b, const Layout &L,
+                                   const ModParams &MP, hipStream_t st) {
+    if (ca) { if (cb) launch_encode_pair<R, CPLX, true, true>(a, b, L, MP, st); else launch_encode_pair<R, CPLX, true, false>(a, b, L, MP, st); }
+    else { if (cb) launch_encode_pair<R, CPLX, false, true>(a, b, L, MP, st); else launch_encode_pair<R, CPLX, false, false>(a, b, L, MP, st); }
 }
 
 bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
                        const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
                        const ModParams &MP, hipStream_t st) {
-    // real operands of one precision (the same ModGroups and tile type); anything else: two launches
-    if (dA.cplx || dB.cplx || dA.dbl != dB.dbl || L.kblk == 0) return false;
-    constexpr int KT = 64;
-    auto operand = [&](const OperandDesc &d, size_t nvec, const int16_t *sft, int8_t *out, size_t plane, size_t vpad) {
+    // operands of one element type (the same ModGroups and tile type); anything else: two launches
+    if (dA.cplx != dB.cplx || dA.dbl != dB.dbl || L.kblk == 0) return false;
+    const bool cplx = dA.cplx;
+    const int KT = cplx ? 32 : 64;
+    // per operand exactly what split_encode sets up for mode 0
+    auto operand = [&](const OperandDesc &d, bool is_A, size_t nvec, const int16_t *sft, int8_t *out, size_t plane) {
         EncOperand e{};
         e.X = d.ptr;
         e.ld = d.ld;
@@ -852,21 +860,24 @@ bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, s
         e.sft = sft;
         e.out = out;
         e.plane = plane;
-        e.vmax = vpad;
-        e.flags = d.contig ? ENC_KFIRST : 0;  // (as launch_encode: k-first block order for contiguous vectors)
+        const bool kara = L.kara;
+        size_t vpad = kara ? (is_A ? L.vsA : L.vsB) : is_A ? (cplx ? L.m_pad - L.m : L.m_pad) : L.n_pad;
         vpad = round_up(vpad, 64);
+        e.vmax = kara ? (is_A ? L.vsA : L.vsB) : is_A ? L.m_pad : L.n_pad;
+        e.flags = (d.contig ? ENC_KFIRST : 0) | (d.conj ? ENC_CONJ : 0) | (kara ? ENC_KARA : 0);
         e.gx = d.contig ? (unsigned)(L.kblk / KT) : (unsigned)(vpad / 64);
         e.gy = d.contig ? (unsigned)(vpad / 64) : (unsigned)(L.kblk / KT);
         return e;
     };
-    const EncOperand a = operand(dA, m, sftA, outA, L.planeA, L.m_pad);
-    const EncOperand b = operand(dB, n, sftB, outB, L.planeB, L.n_pad);
+    const EncOperand a = operand(dA, true, m, sftA, outA, L.planeA);
+    const EncOperand b = operand(dB, false, n, sftB, outB, L.planeB);
+    if (a.gx * a.gy == 0 || b.gx * b.gy == 0) return false;
     if (dA.dbl) {
-        if (dA.contig) { if (dB.contig) launch_encode_pair<double, true, true>(a, b, L, MP, st); else launch_encode_pair<double, true, false>(a, b, L, MP, st); }
-        else { if (dB.contig) launch_encode_pair<double, false, true>(a, b, L, MP, st); else launch_encode_pair<double, false, false>(a, b, L, MP, st); }
+        if (cplx) launch_encode_pair_ops<double, true>(dA.contig, dB.contig, a, b, L, MP, st);
+        else launch_encode_pair_ops<double, false>(dA.contig, dB.contig, a, b, L, MP, st);
     } else {
-        if (dA.contig) { if (dB.contig) launch_encode_pair<float, true, true>(a, b, L, MP, st); else launch_encode_pair<float, true, false>(a, b, L, MP, st); }
-        else { if (dB.contig) launch_encode_pair<float, false, true>(a, b, L, MP, st); else launch_encode_pair<float, false, false>(a, b, L, MP, st); }
+        if (cplx) launch_encode_pair_ops<float, true>(dA.contig, dB.contig, a, b, L, MP, st);
+        else launch_encode_pair_ops<float, false>(dA.contig, dB.contig, a, b, L, MP, st);
     }
     return true;
 }
