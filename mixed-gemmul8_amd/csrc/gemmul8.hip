@@ -105,7 +105,12 @@ struct LaneGuard {
         // the fork / join costs ~10 us of stream latency: worth it from (m + n) k = 2^25 up
         // (4096^3: split 0.228 -> 0.206 ms; 1024^3: 39 -> 50 us with the lane, so none there)
         const bool big = (c.m + c.n) * c.k >= ((size_t)1 << 25);
-        c.lane = big ? lanes::acquire(c.st) : nullptr;
+        // real f64 A (op N) x B (op N) in fast mode runs both operands in each split launch instead (the
+        // pair kernels, phase_split): at 8192^3 split 0.757 -> 0.735 ms, at 4096^3 the same.  Other forms
+        // keep the two streams (their shift passes stay per operand).
+        const bool pairs = c.fast && !c.A.cplx && !c.B.cplx && c.A.dbl && c.B.dbl && !c.A.contig && c.B.contig &&
+                           c.VT == 128 && (c.slice_planes == 0 || c.slice_planes >= c.N);
+        c.lane = big && !pairs ? lanes::acquire(c.st) : nullptr;
         c.stB = c.lane ? c.lane->s : c.st;
     }
     ~LaneGuard() {

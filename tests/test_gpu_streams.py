@@ -43,7 +43,8 @@ def _inputs(m, n, k, seed, dtype=torch.float64):
     (torch.complex128, 1, False, None, False),   # COMPLEX_BIG_MATRIX_ENCODE, accurate (bound of 2m rows)
     (torch.complex128, 3, True, None, False),    # COMPLEX_KARATSUBA_MULT
     (torch.float64, 0, False, 4, False),         # low-memory mode: moduli in groups of 4
-    # (m + n) k >= 2^25: operand B's split runs on the second stream (fork / join in the graph)
+    # (m + n) k >= 2^25: accurate mode runs operand B's split on the second stream (fork / join in the
+    # graph); fast mode with one element type runs the pair split kernels on the call's stream
     (torch.float64, 0, True, None, True),
     (torch.float64, 0, False, None, True),
     (torch.float64, 0, False, 4, True),
