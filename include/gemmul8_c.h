@@ -11,6 +11,9 @@
  * All device pointers are column-major HIP device memory; alpha/beta are host
  * pointers to one TC value; the work buffer is caller-owned (>= work size).
  * Return codes: 0 ok, GEMMUL8_E_* < 0 on invalid arguments (nothing enqueued).
+ * GEMMUL8_E_HIP: a kernel launch of THIS call failed; the phases after it were not enqueued
+ * (C is written only by the last phase).  An error left pending on the calling thread by
+ * earlier HIP calls is cleared at entry, not reported as the call's own.
  */
 #ifndef GEMMUL8_C_H
 #define GEMMUL8_C_H

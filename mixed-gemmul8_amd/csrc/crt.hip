@@ -130,8 +130,14 @@ template <> struct BlasEpi<1> {
         return epi_f(v, c, (float)a.ar, (float)a.br);
     }
 };
+// Complex outputs.  With real alpha and beta (ai = bi = 0) each component takes the real-scalar form,
+// so a non-finite Im(C) cannot reach Re(C) through a 0 * Inf term; for finite values it gives the bits
+// of the full complex form (whose zero-imaginary terms only add signed zeros), and for alpha = beta = 1
+// it is the reference's component-wise CAdd (inverse_scaling.hpp:370-392).
 template <> struct BlasEpi<2> {
     static __device__ __forceinline__ double2 f(double2 v, double2 c, const CrtArgs &a) {
+        if (a.ai == 0.0 && a.bi == 0.0)
+            return make_double2(__builtin_fma(a.br, c.x, a.ar * v.x), __builtin_fma(a.br, c.y, a.ar * v.y));
         const double tr = __builtin_fma(a.ar, v.x, -a.ai * v.y), ti = __builtin_fma(a.ar, v.y, a.ai * v.x);
         return make_double2(__builtin_fma(a.br, c.x, __builtin_fma(-a.bi, c.y, tr)),
                             __builtin_fma(a.br, c.y, __builtin_fma(a.bi, c.x, ti)));
@@ -140,6 +146,8 @@ template <> struct BlasEpi<2> {
 template <> struct BlasEpi<3> {
     static __device__ __forceinline__ float2 f(float2 v, float2 c, const CrtArgs &a) {
         const float arf = (float)a.ar, aif = (float)a.ai, brf = (float)a.br, bif = (float)a.bi;
+        if (aif == 0.0f && bif == 0.0f)
+            return make_float2(__builtin_fmaf(brf, c.x, arf * v.x), __builtin_fmaf(brf, c.y, arf * v.y));
         const float tr = __builtin_fmaf(arf, v.x, -aif * v.y), ti = __builtin_fmaf(arf, v.y, aif * v.x);
         return make_float2(__builtin_fmaf(brf, c.x, __builtin_fmaf(-bif, c.y, tr)),
                            __builtin_fmaf(brf, c.y, __builtin_fmaf(bif, c.x, ti)));

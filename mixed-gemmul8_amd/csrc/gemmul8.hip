@@ -58,23 +58,30 @@ static bool disabled() {  // GEMMUL8_SINGLE_STREAM=1: everything on the caller's
     }();
     return d;
 }
+static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone;
+}
 static Lane *acquire(hipStream_t st) {
     if (disabled()) return nullptr;
+    // a call captured into a graph runs on the caller's stream alone: a lane forked into the capture
+    // would stay part of it until the origin stream ends the capture, long after this call returns
+    // it to the pool, and an eager call of another thread taking it meanwhile would be recorded into
+    // the foreign graph.  So capture is tested before the pool is looked at.
+    if (capturing(st)) return nullptr;
     int dev = 0;
     if (hipStreamGetDevice(st, &dev) != hipSuccess) return nullptr;
     {
         std::lock_guard<std::mutex> g(mu);
         for (size_t i = 0; i < free_list.size(); ++i)
-            if (free_list[i]->dev == dev) {
+            // a pooled lane still joined to somebody's capture is skipped (left in the pool)
+            if (free_list[i]->dev == dev && !capturing(free_list[i]->s)) {
                 Lane *l = free_list[i];
                 free_list[i] = free_list.back();
                 free_list.pop_back();
                 return l;
             }
     }
-    // no new streams or events while the caller captures a graph (the call then runs on one stream)
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) return nullptr;
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) return nullptr;
     if (cur != dev && hipSetDevice(dev) != hipSuccess) return nullptr;
@@ -171,6 +178,11 @@ static void resolve_all() {
 }
 }  // namespace timing
 
+// Launch errors: every entry point that enqueues work first clears an error left pending on the
+// calling thread by earlier, unrelated HIP calls (hipGetLastError would otherwise report it as
+// ours), then checks after each phase, so GEMMUL8_E_HIP always means a launch of THIS call failed
+// and no later phase was enqueued.
+static inline void clear_stale_error() { (void)hipGetLastError(); }
 static inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
 static bool is_capturing(hipStream_t st) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -319,11 +331,22 @@ static int run(Call &c, double *phase_ns) {
     }
     if (record) (void)hipEventRecord(rec.start, c.st);
 
+    // a failed launch ends the call before the next phase is enqueued (the events recorded so far
+    // go back to the pool unread)
+    auto fail = [&]() {
+        if (record) {
+            std::lock_guard<std::mutex> g(timing::mu);
+            timing::pool.push_back(rec);
+        }
+        return GEMMUL8_E_HIP;
+    };
     const unsigned S = v.L.S;
     if (S >= c.N) {
         phase_split(c, v, 0, c.N, false);
+        if (!launch_ok()) return fail();
         if (record) (void)hipEventRecord(rec.ev[0], c.st);
         phase_products(v, c.N, 0, c.N, 0, c.st);
+        if (!launch_ok()) return fail();
     } else {
         // low-memory mode: the moduli in groups of S through the same S slice planes (each group
         // re-reads A and B); the product phase timer then includes the re-encoding
@@ -332,6 +355,7 @@ static int run(Call &c, double *phase_ns) {
         operand_shifts(c, v, true, c.st);
         operand_shifts(c, v, false, c.stB);
         join(c);
+        if (!launch_ok()) return fail();
         if (record) (void)hipEventRecord(rec.ev[0], c.st);
         for (unsigned j0 = 0; j0 < c.N; j0 += S) {
             const unsigned j1 = j0 + S < c.N ? j0 + S : c.N;
@@ -339,7 +363,9 @@ static int run(Call &c, double *phase_ns) {
             operand_encode(c, v, true, j0, j1, 0, c.st);
             operand_encode(c, v, false, j0, j1, 0, c.stB);
             join(c);
+            if (!launch_ok()) return fail();
             phase_products(v, c.N, j0, j1, 0, c.st);
+            if (!launch_ok()) return fail();
         }
     }
     if (record) {
@@ -348,8 +374,8 @@ static int run(Call &c, double *phase_ns) {
     }
 
     phase_crt(v, c.N, c.ot, c.alpha, c.beta, c.C, c.ldc, c.st);
+    if (!launch_ok()) return fail();
     if (record) (void)hipEventRecord(rec.ev[3], c.st);
-    if (!launch_ok()) return GEMMUL8_E_HIP;
 
     if (want_events) {
         (void)hipEventSynchronize(rec.ev[3]);
@@ -432,6 +458,7 @@ int gemmul8_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k,
                                 ldc, num_moduli, fastmode, work, compute_type, c);
     if (rc != GEMMUL8_OK) return rc;
     if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
     return oz2::run(c, phase_ns);
 }
 
@@ -451,6 +478,7 @@ int gemmul8_gemm_lowmem(void *stream, int op_a, int op_b, size_t m, size_t n, si
     if (rc != GEMMUL8_OK) return rc;
     c.slice_planes = slice_planes;
     if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
     return oz2::run(c, phase_ns);
 }
 
@@ -462,6 +490,7 @@ int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, si
                                 nullptr, m, num_moduli, 0, work, compute_type, c);
     if (rc != GEMMUL8_OK) return rc;
     if (m == 0 && n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, c.cplx);
     if (m == 0 || n == 0) {  // an empty block contributes nothing to the other operand's maxima
         oz2::zero_i32(v.bound, v.L.bm_pad + v.L.bn_pad, c.st);
@@ -481,6 +510,7 @@ int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k
     if (rc != GEMMUL8_OK) return rc;
     if (mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
     if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
     oz2::LaneGuard lane(c);
     oz2::phase_split(c, oz2::views(work, m, n, k, num_moduli, c.cplx), mod_begin, mod_end,
                      (flags & GEMMUL8_SPLIT_BOUND_READY) != 0);
@@ -492,6 +522,7 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
     if (num_moduli < 2 || num_moduli > 20 || mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
     if (compute_type < GEMMUL8_REAL_DEFAULT || compute_type > GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_TYPES;
     if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
     hipStream_t st = static_cast<hipStream_t>(stream);
     // with timing enabled the launch is bracketed like gemmul8_gemm's product phase (phases 0/3 read 0)
@@ -526,6 +557,7 @@ int gemmul8_recombine(void *stream, size_t m, size_t n, size_t k, unsigned num_m
     if (compute_type < GEMMUL8_REAL_DEFAULT || compute_type > GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_TYPES;
     if (ldc < m) return GEMMUL8_E_SIZE;
     if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, cp);
     oz2::phase_crt(v, num_moduli, static_cast<oz2::OutType>(type_c), alpha, beta, C, ldc,
                    static_cast<hipStream_t>(stream));
@@ -563,6 +595,7 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
     const oz2::Layout L = oz2::make_layout(m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
     int8_t *base = static_cast<int8_t *>(work);
     const oz2::ModParams MP = oz2::make_mod_params(num_moduli);
+    oz2::clear_stale_error();
     oz2::gemm_i8(base + L.offA, base + L.offB, L, 1, oz2::Epi::RAW, C32, nullptr, nullptr, MP,
                  static_cast<hipStream_t>(stream));
     return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;

@@ -17,7 +17,16 @@
 //   GEMMUL8_INTERCEPT_THRESHOLD_M / _N / _K   emulate only when m, n, k are all >= (default 128)
 //   GEMMUL8_INFO=1                one line per call on stderr
 // Calls with device-resident alpha/beta (pointer mode device), sizes below the thresholds or
-// arguments the emulator rejects go to the vendor routine unchanged.
+// arguments the emulator rejects (nothing enqueued) go to the vendor routine unchanged.  A call
+// whose kernels were enqueued and then failed to launch is never forwarded (the vendor routine
+// would apply beta to a C the emulator may already have written): it returns an execution error.
+//
+// Workspaces: an eager call uses one buffer per (device, stream), grown on demand (calls on one
+// stream are ordered, so reuse is safe).  A call captured into a graph never uses that buffer (a
+// later, larger eager call would free it under the graph, and graphs captured on one stream would
+// share it and race when replayed on different streams): each (device, capture, stream) gets a
+// buffer of its own, allocated during the capture under relaxed capture mode and never freed,
+// since the graph may be replayed at any time.
 //
 // The interposer has no link-time dependency on the HIP runtime or the BLAS libraries: a
 // preloaded object that pulled in its own libamdhip64 would put a second HIP runtime into a
@@ -30,6 +39,7 @@
 #include <hipblas/hipblas.h>
 #include <rocblas/rocblas.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -37,6 +47,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <utility>
 
 #include "../../include/gemmul8_c.h"
@@ -51,6 +62,8 @@ struct Api {
     decltype(&hipFree) free_ = nullptr;
     decltype(&hipStreamSynchronize) streamSync = nullptr;
     decltype(&hipStreamIsCapturing) isCapturing = nullptr;
+    decltype(&hipStreamGetCaptureInfo) captureInfo = nullptr;
+    decltype(&hipThreadExchangeStreamCaptureMode) exchangeCaptureMode = nullptr;
     decltype(&hipblasGetStream) hbGetStream = nullptr;
     decltype(&hipblasGetPointerMode) hbGetPointerMode = nullptr;
     decltype(&rocblas_get_stream) rbGetStream = nullptr;
@@ -75,6 +88,9 @@ struct Api {
         free_ = reinterpret_cast<decltype(free_)>(sym(hip, "hipFree"));
         streamSync = reinterpret_cast<decltype(streamSync)>(sym(hip, "hipStreamSynchronize"));
         isCapturing = reinterpret_cast<decltype(isCapturing)>(sym(hip, "hipStreamIsCapturing"));
+        captureInfo = reinterpret_cast<decltype(captureInfo)>(sym(hip, "hipStreamGetCaptureInfo"));
+        exchangeCaptureMode =
+            reinterpret_cast<decltype(exchangeCaptureMode)>(sym(hip, "hipThreadExchangeStreamCaptureMode"));
         hbGetStream = reinterpret_cast<decltype(hbGetStream)>(sym(hipblas, "hipblasGetStream"));
         hbGetPointerMode = reinterpret_cast<decltype(hbGetPointerMode)>(sym(hipblas, "hipblasGetPointerMode"));
         rbGetStream = reinterpret_cast<decltype(rbGetStream)>(sym(rocblas, "rocblas_get_stream"));
@@ -157,20 +173,43 @@ const Config &cfg() {
     return c;
 }
 
-// one workspace per (device, stream): calls on one stream are ordered, so reuse is safe
+std::atomic<void *> last_workspace{nullptr};  // test hook: gemmul8_hijack_last_workspace()
+
+// workspace of one call (see the header comment); nullptr: none available, forward the call
 void *workspace(size_t bytes, hipStream_t st) {
     static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> pool;
+    static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> eager;
+    // (device, capture id, stream) -> the capture's current buffer; every buffer ever handed to a
+    // capture stays allocated (the graph's nodes hold its address)
+    static std::map<std::tuple<int, unsigned long long, hipStream_t>, std::pair<void *, size_t>> captured;
     const Api &a = api();
     int dev = 0;
     (void)a.getDevice(&dev);
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    unsigned long long id = 0;
+    if (a.captureInfo) {
+        if (a.captureInfo(st, &cap, &id) != hipSuccess) return nullptr;
+    } else if (a.isCapturing && a.isCapturing(st, &cap) != hipSuccess) {
+        return nullptr;
+    }
     std::lock_guard<std::mutex> g(mu);
-    auto &e = pool[{dev, st}];
+    if (cap != hipStreamCaptureStatusNone) {
+        if (cap != hipStreamCaptureStatusActive || !a.captureInfo || !a.exchangeCaptureMode) return nullptr;
+        auto &e = captured[{dev, id, st}];
+        if (e.second >= bytes) return e.first;
+        // an allocation is not a stream operation, but global capture mode forbids it as "unsafe":
+        // relaxed mode for this thread around it (as PyTorch's caching allocator does)
+        hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+        (void)a.exchangeCaptureMode(&mode);
+        void *p = nullptr;
+        const bool ok = a.malloc_(&p, bytes) == hipSuccess;
+        (void)a.exchangeCaptureMode(&mode);
+        if (!ok) return nullptr;
+        e = {p, bytes};  // a smaller earlier buffer of this capture stays allocated
+        return p;
+    }
+    auto &e = eager[{dev, st}];
     if (e.second < bytes) {
-        // growing the workspace synchronises and allocates: not while the stream is captured into a
-        // graph (the call is forwarded to the vendor routine instead)
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (a.isCapturing && (a.isCapturing(st, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone)) return nullptr;
         if (e.first) {
             (void)a.streamSync(st);
             (void)a.free_(e.first);
@@ -185,22 +224,29 @@ void *workspace(size_t bytes, hipStream_t st) {
 
 int op_code(int op) { return op == 111 ? GEMMUL8_OP_N : (op == 112 ? GEMMUL8_OP_T : GEMMUL8_OP_C); }
 
-// true when the call was emulated
-bool emulate(const char *fn, const Mode &md, hipStream_t st, int opa, int opb, long m, long n, long k, int type,
-             const void *alpha, const void *A, long lda, const void *B, long ldb, const void *beta, void *C, long ldc) {
+enum class Outcome { emulated, forward, failed };
+
+// emulated: done; forward: nothing was enqueued, the vendor routine takes the call; failed: the
+// emulator's kernels were enqueued and a launch failed (never forwarded)
+Outcome emulate(const char *fn, const Mode &md, hipStream_t st, int opa, int opb, long m, long n, long k, int type,
+                const void *alpha, const void *A, long lda, const void *B, long ldb, const void *beta, void *C,
+                long ldc) {
     const Config &c = cfg();
-    if (!md.on || m < c.tm || n < c.tn || k < c.tk || !api().ok) return false;
+    if (!md.on || m < c.tm || n < c.tn || k < c.tk || !api().ok) return Outcome::forward;
     const bool cplx = type == GEMMUL8_C_64F || type == GEMMUL8_C_32F;
     const int ct = cplx ? c.ctype : GEMMUL8_REAL_DEFAULT;
     const size_t ws = api().workSize(m, n, k, md.N, ct);
     void *work = ws ? workspace(ws, st) : nullptr;
-    if (!work) return false;
+    if (!work) return Outcome::forward;
+    last_workspace.store(work);
     const int rc = api().gemm(st, op_code(opa), op_code(opb), m, n, k, type, type, type, alpha, A, lda, B, ldb, beta,
                                 C, ldc, md.N, md.fast, work, ct, nullptr);
+    const Outcome o = rc == GEMMUL8_OK ? Outcome::emulated : (rc == GEMMUL8_E_HIP ? Outcome::failed : Outcome::forward);
     if (c.info)
         fprintf(stderr, "[gemmul8] %s m=%ld n=%ld k=%ld -> %s (num_moduli=%u, %s)\n", fn, m, n, k,
-                rc == GEMMUL8_OK ? "emulated" : "forwarded", md.N, md.fast ? "fast" : "accurate");
-    return rc == GEMMUL8_OK;
+                o == Outcome::emulated ? "emulated" : (o == Outcome::failed ? "launch failed" : "forwarded"), md.N,
+                md.fast ? "fast" : "accurate");
+    return o;
 }
 
 // the vendor definition: in the application's hipBLAS / rocBLAS, else the next one in the global scope
@@ -234,10 +280,12 @@ bool host_stream(rocblas_handle h, hipStream_t *st) {
                          T *C, int ldc) {                                                                          \
         static auto real = next_symbol<decltype(&NAME)>(#NAME);                                                    \
         hipStream_t st = nullptr;                                                                                  \
-        if (host_stream(handle, &st) &&                                                                            \
-            emulate(#NAME, cfg().MODE, st, (int)transA, (int)transB, m, n, k, TYPE, alpha, A, lda, B, ldb, beta,  \
-                    C, ldc))                                                                                       \
-            return HIPBLAS_STATUS_SUCCESS;                                                                         \
+        if (host_stream(handle, &st)) {                                                                            \
+            const Outcome o = emulate(#NAME, cfg().MODE, st, (int)transA, (int)transB, m, n, k, TYPE, alpha, A,   \
+                                      lda, B, ldb, beta, C, ldc);                                                  \
+            if (o == Outcome::emulated) return HIPBLAS_STATUS_SUCCESS;                                             \
+            if (o == Outcome::failed) return HIPBLAS_STATUS_EXECUTION_FAILED;                                      \
+        }                                                                                                          \
         return real ? real(handle, transA, transB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc)                  \
                     : HIPBLAS_STATUS_NOT_SUPPORTED;                                                                \
     }
@@ -251,10 +299,12 @@ bool host_stream(rocblas_handle h, hipStream_t *st) {
         hipStream_t st = nullptr;                                                                                  \
         int b = 0;                                                                                                 \
         if (batchCount > 0 && host_stream(handle, &st))                                                           \
-            for (; b < batchCount; ++b)                                                                            \
-                if (!emulate(#NAME, cfg().MODE, st, (int)transA, (int)transB, m, n, k, TYPE, alpha,               \
-                             A + b * strideA, lda, B + b * strideB, ldb, beta, C + b * strideC, ldc))             \
-                    break;                                                                                         \
+            for (; b < batchCount; ++b) {                                                                          \
+                const Outcome o = emulate(#NAME, cfg().MODE, st, (int)transA, (int)transB, m, n, k, TYPE, alpha,  \
+                                          A + b * strideA, lda, B + b * strideB, ldb, beta, C + b * strideC, ldc); \
+                if (o == Outcome::failed) return HIPBLAS_STATUS_EXECUTION_FAILED;                                  \
+                if (o == Outcome::forward) break;                                                                  \
+            }                                                                                                      \
         if (b == batchCount && batchCount > 0) return HIPBLAS_STATUS_SUCCESS;                                      \
         /* the batches not emulated (all of them, or those after a rejected one) go to the vendor routine */     \
         return real ? real(handle, transA, transB, m, n, k, alpha, A + b * strideA, lda, strideA, B + b * strideB, \
@@ -263,6 +313,10 @@ bool host_stream(rocblas_handle h, hipStream_t *st) {
     }
 
 extern "C" {
+// the workspace the interposer handed to its latest emulated call (tests check that a captured
+// call never shares the eager buffer of its stream)
+void *gemmul8_hijack_last_workspace(void) { return last_workspace.load(); }
+
 OZ2_HIPBLAS_GEMM(hipblasDgemm, double, GEMMUL8_R_64F, d)
 OZ2_HIPBLAS_GEMM(hipblasZgemm, hipDoubleComplex, GEMMUL8_C_64F, d)
 OZ2_HIPBLAS_GEMM(hipblasSgemm, float, GEMMUL8_R_32F, s)
@@ -278,10 +332,12 @@ OZ2_HIPBLAS_GEMM_SB(hipblasZgemmStridedBatched, hipDoubleComplex, GEMMUL8_C_64F,
                         rocblas_int ldb, const T *beta, T *C, rocblas_int ldc) {                                  \
         static auto real = next_symbol<decltype(&NAME)>(#NAME);                                                    \
         hipStream_t st = nullptr;                                                                                  \
-        if (host_stream(handle, &st) &&                                                                            \
-            emulate(#NAME, cfg().MODE, st, (int)transA, (int)transB, m, n, k, TYPE, alpha, A, lda, B, ldb, beta,  \
-                    C, ldc))                                                                                       \
-            return rocblas_status_success;                                                                         \
+        if (host_stream(handle, &st)) {                                                                            \
+            const Outcome o = emulate(#NAME, cfg().MODE, st, (int)transA, (int)transB, m, n, k, TYPE, alpha, A,   \
+                                      lda, B, ldb, beta, C, ldc);                                                  \
+            if (o == Outcome::emulated) return rocblas_status_success;                                             \
+            if (o == Outcome::failed) return rocblas_status_internal_error;                                        \
+        }                                                                                                          \
         return real ? real(handle, transA, transB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc)                  \
                     : rocblas_status_not_implemented;                                                              \
     }

@@ -599,6 +599,11 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
                     double cr = zb ? 0.0 : Cz[2 * o], ci = zb ? 0.0 : Cz[2 * o + 1];
                     if (al[0] == 1.0 && al[1] == 0.0 && be[0] == 0.0 && be[1] == 0.0) {
                         Cz[2 * o] = vr; Cz[2 * o + 1] = vi;
+                    } else if (al[1] == 0.0 && be[1] == 0.0) {
+                        /* real alpha, beta: per component (alpha = beta = 1 is the reference's CAdd,
+                         * inverse_scaling.hpp:370-392); no 0*Inf from Im(C) into Re(C) */
+                        Cz[2 * o] = fma(be[0], cr, al[0] * vr);
+                        Cz[2 * o + 1] = fma(be[0], ci, al[0] * vi);
                     } else { /* alpha*v + beta*c, products fused as the GPU build does */
                         double tr = fma(al[0], vr, -al[1] * vi), ti = fma(al[0], vi, al[1] * vr);
                         Cz[2 * o] = fma(be[0], cr, fma(-be[1], ci, tr));
@@ -612,6 +617,9 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
                     float cr = zb ? 0.0f : Cc[2 * o], ci = zb ? 0.0f : Cc[2 * o + 1];
                     if (al[0] == 1.0f && al[1] == 0.0f && be[0] == 0.0f && be[1] == 0.0f) {
                         Cc[2 * o] = fr; Cc[2 * o + 1] = fi;
+                    } else if (al[1] == 0.0f && be[1] == 0.0f) {
+                        Cc[2 * o] = fmaf(be[0], cr, al[0] * fr);
+                        Cc[2 * o + 1] = fmaf(be[0], ci, al[0] * fi);
                     } else {
                         float tr = fmaf(al[0], fr, -al[1] * fi), ti = fmaf(al[0], fi, al[1] * fr);
                         Cc[2 * o] = fmaf(be[0], cr, fmaf(-be[1], ci, tr));

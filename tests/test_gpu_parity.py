@@ -524,3 +524,45 @@ def test_integer_inputs_at_scale(fast):
     Wc = G.alloc_work(mc, nc, kc, 12, G.COMPLEX_BIG_MATRIX_ENCODE)
     G.gemm(0, 0, mc, nc, kc, 1.0, Ac, mc, Bc, kc, 0.0, Cc, mc, 12, fast, Wc, G.COMPLEX_BIG_MATRIX_ENCODE)
     check(Cc, Bc @ Ac, 2.0 * (Bc.abs() @ Ac.abs()))
+
+
+@pytest.mark.parametrize("dt", [np.complex128, np.complex64])
+@pytest.mark.parametrize("alpha,beta", [(1.0, 1.0), (2.0, 0.5), (1.0, -3.0)])
+def test_complex_nonfinite_imag_c(dt, alpha, beta):
+    """Real alpha and beta on a complex C whose imaginary parts hold Inf / NaN: each component takes
+    the real-scalar form (alpha = beta = 1 is the reference's component-wise CAdd,
+    inverse_scaling.hpp:370-392), so Re(C) stays finite where Re(C0) is; bits equal to the oracle."""
+    rng = np.random.default_rng(404 + (dt == np.complex64))
+    m, n, k = 40, 30, 50
+    A, B = randmat_np(rng, m, k, dtype=dt), randmat_np(rng, k, n, dtype=dt)
+    C0 = randmat_np(rng, m, n, dtype=dt)
+    C0.imag[3, 4] = np.inf
+    C0.imag[7, 1] = -np.inf
+    C0.imag[0, 0] = np.inf
+    C, Co = check_full(A, B, 9, alpha=alpha, beta=beta, C0=C0)
+    assert np.isfinite(C.real).all()
+    assert np.isinf(C.imag[3, 4]) and np.isinf(C.imag[7, 1])
+
+
+def test_stale_hip_error_is_not_reported():
+    """An error left pending on the thread by an earlier, unrelated HIP call (here a failed
+    hipSetDevice) is cleared at entry: the call succeeds and writes the correct bits with beta != 0
+    (it used to return GEMMUL8_E_HIP after writing C, and the interposer then forwarded it)."""
+    import ctypes
+    torch = _torch()
+    hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
+    rng = np.random.default_rng(77)
+    m, n, k = 96, 80, 130
+    A, B, C0 = randmat_np(rng, m, k), randmat_np(rng, k, n), randmat_np(rng, m, n)
+    from oracle import oracle as O
+    Co = O.gemm(A, B, 14, True, np.float64, 1.0, 0.5, C0)
+    import gemmul8 as G
+    dA, dB, dC = to_dev(A), to_dev(B), to_dev(C0)
+    work = G.alloc_work(m, n, k, 14)
+    torch.cuda.synchronize()
+    assert hip.hipSetDevice(ctypes.c_int(12345)) != 0
+    assert hip.hipPeekAtLastError() != 0  # the stale error is pending
+    G.gemm(0, 0, m, n, k, 1.0, dA, m, dB, k, 0.5, dC, m, 14, True, work)  # raises on a nonzero return
+    torch.cuda.synchronize()
+    assert hip.hipPeekAtLastError() == 0
+    assert bits_equal(np.asfortranarray(dC.cpu().numpy().T), Co)

@@ -125,3 +125,36 @@ def test_two_threads_two_streams_same_bits():
     for j in jobs:
         assert _same(j["C"], j["ref"])
     assert np.isfinite(jobs[0]["C"].cpu().numpy()).all()
+
+
+def test_eager_call_during_foreign_capture_gets_no_captured_lane():
+    """Operand B's split runs on a pooled second stream (a "lane") for big non-pair forms.  A call
+    captured into a graph must not take a lane: forked into the capture, the lane stays part of it
+    until the capture ends, and an eager call that picked it from the pool meanwhile would record
+    its B split into the foreign graph instead of running it.  Deterministic form: an eager call on
+    another stream while the capture is still open (relaxed capture mode)."""
+    m, n, k, N = 2048, 2040, 8192, 14  # (m + n) k >= 2^25, accurate mode: the two-stream split
+    A, B = _inputs(m, n, k, 21)
+    A2, B2 = _inputs(m, n, k, 23)
+    W, W2 = G.alloc_work(m, n, k, N), G.alloc_work(m, n, k, N)
+    C_ref2 = torch.zeros((n, m), dtype=torch.float64, device="cuda")
+    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A2, m, B2, k, 0.0, C_ref2, m, N, False, W2)  # leaves a lane in the pool
+    C_ref = torch.zeros_like(C_ref2)
+    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C_ref, m, N, False, W)
+    torch.cuda.synchronize()
+    C = torch.zeros_like(C_ref)
+    C2 = torch.zeros_like(C_ref2)
+    s, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, False, W, stream=s)
+            # still capturing on s: an eager call on s2 takes a lane from the pool
+            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A2, m, B2, k, 0.0, C2, m, N, False, W2, stream=s2)
+    torch.cuda.synchronize()
+    assert _same(C2, C_ref2)  # the eager call ran in full (its B split was not recorded into g)
+    W.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    assert _same(C, C_ref)
