@@ -203,7 +203,7 @@ def main():
         achieved = ops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
         roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(INT8_PEAK_TOPS, 1),
                     "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4), "traffic": traffic_from_profile((m, n, k, planes, not args.accurate)),
-                    "kernel": "gemm_i8_kernel<RESIDUE> (int8 ops counted as FLOP, 2*m*n*k*num_moduli per launch)",
+                    "kernel": "gemm_i8_persistent_kernel (residue products; int8 ops counted as FLOP, 2*m*n*k*num_moduli per launch)",
                     "avg_launch_ms": round(gemm_ms, 4)}
         # measured live after the timed region: the same MFMA alone on uniformly random operand bytes
         # (the residue distribution) in registers -- the clock the chip holds under that load bounds

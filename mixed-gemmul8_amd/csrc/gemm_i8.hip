@@ -76,6 +76,11 @@ struct GemmArgs {
     // these strides in the A, B and output planes
     unsigned nsub;
     size_t subA, subB, subOut;
+    // persistent kernel: planes of the launch (sub-products counted) and the bytes of the A and B
+    // regions its buffer descriptors cover (< 4 GiB)
+    unsigned nplanes;
+    uint32_t regionA, regionB;
+    uint32_t *queue;  // 8 per-XCD tile-queue heads, zeroed before the launch
 };
 
 // One 16-byte-per-lane LDS-DMA: LDS[m0 + lane*16] <- gsrc (per lane).  Issued from inline asm
@@ -85,7 +90,8 @@ struct GemmArgs {
 #define OZ2_ABLATE 0  // probe builds only: 1 = no LDS-DMA, 2 = no MFMA, 3 = no LDS reads, 5 = LDS reads of the first
                      // step only, 6 = LDS-DMA of the prologue only (real operands, no data movement in the loop),
                      // 7 = residue epilogue reduced to the low byte, 8 = every LDS-DMA re-reads k-steps 0/1
-                     // (L2 hits: the fabric / Infinity-Cache share of the DMA)
+                     // (L2 hits: the fabric / Infinity-Cache share of the DMA), 9 = residues parked in LDS but
+                     // not stored, 10 = no epilogue (accumulators kept live)
 #endif
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_addr) {
     if (OZ2_ABLATE == 1) return;
@@ -326,6 +332,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I
             const int pm = x & 3;
             uint4 *dst = reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd);
             uint4 res = make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+            if (OZ2_ABLATE == 9) {  // probe: no residue store
+                asm volatile("" ::"v"(res.x), "v"(res.y), "v"(res.z), "v"(res.w));
+                continue;
+            }
             if constexpr (EPI == EPI_RESIDUE_ADD) {  // k-chunked product: (earlier chunks + this chunk) mod p
                 const uint4 prev = *dst;
                 res = make_uint4(add_mod_bytes(res.x, prev.x, (uint32_t)p), add_mod_bytes(res.y, prev.y, (uint32_t)p),
@@ -494,9 +504,238 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
     }
     barrier();  // all waves done with the ring before the epilogue reuses it
 
+    if (OZ2_ABLATE == 10) {  // probe: no epilogue
+#pragma unroll
+        for (int i = 0; i < ACC_I; ++i)
+#pragma unroll
+            for (int jj = 0; jj < ACC_J; ++jj) asm volatile("" ::"v"(acc[i][jj]));
+        return;
+    }
     epilogue<EPI>(g, acc, smem, tid, lane, wr, wc, tm, tn, j, sb, true);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent form of the residue product (buffer DMA; real operands and Karatsuba sub-products).
+// One block per CU.  The k-steps of a block's consecutive tiles form ONE pipeline: the LDS-DMA
+// runs D steps ahead across tile boundaries, so the next tile's first panels land while the
+// current tile finishes and its epilogue runs (the one-tile kernel pays that first-data latency,
+// the block teardown and the next block's launch once per tile).  The epilogue parks the residues
+// in the ring slot of the tile's last step plus a spare 32 KiB and issues the 8 residue stores per
+// wave without waiting for them: they stay in flight under the next tile's first two k-steps (the
+// vmcnt waits there count them as younger than the awaited DMA; from the third step on they are
+// older and complete first).
+// Tiles come from one queue per XCD (head counters zeroed before the launch), in the order the
+// hardware dispatcher hands the one-tile kernel's blocks to that XCD: plane by plane, the XCD's
+// contiguous share of each plane's grouped raster.  So the ~32 tiles in flight on an XCD are always
+// neighbours and share 4 A and 8 B panels in its L2.  (A static tile list per block was measured:
+// the blocks drift apart over the launch and the L2 hit rate fell from 79 % to 69 %.)  The first
+// tile of a block is its slot on the XCD, the second is dequeued at the start, every later one in
+// the epilogue two tiles ahead, so the DMA cursor always knows the tile it runs into.
+constexpr int PARK_SPARE = 32768;
+constexpr int PARK_STORES = 4096 / NTHREADS;  // 16-byte residue stores per thread (and per wave) per tile
+constexpr unsigned NO_TILE = 0xffffffffu;
+
+struct TileRef {
+    unsigned j, sb, tm, tn;
+    uint32_t offA, offB;  // byte offsets of the tile's k-step 0 panel in the A and B regions
+};
+
+template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArgs &g, unsigned u) {
+    constexpr unsigned GM = 4;
+    const unsigned P = g.mtiles * g.ntiles;
+    const unsigned y = u / P, v = u - y * P;
+    TileRef t;
+    t.j = SUB ? y / 3 : y;
+    t.sb = SUB ? y - 3 * t.j : 0;
+    const unsigned grp = v / (GM * g.ntiles);
+    const unsigned gm = min(GM, g.mtiles - grp * GM);
+    const unsigned idx = v - grp * GM * g.ntiles;
+    t.tm = grp * GM + idx % gm;
+    t.tn = idx / gm;
+    t.offA = (uint32_t)(t.j * g.planeA + t.sb * g.subA + (size_t)t.tm * g.kstride * PANEL);
+    t.offB = (uint32_t)(t.j * g.planeB + t.sb * g.subB + (size_t)t.tn * g.kstride * PANEL);
+    // block-uniform: keep them in SGPRs (the compiler's divergence analysis does not see it)
+    t.j = __builtin_amdgcn_readfirstlane(t.j);
+    t.sb = __builtin_amdgcn_readfirstlane(t.sb);
+    t.tm = __builtin_amdgcn_readfirstlane(t.tm);
+    t.tn = __builtin_amdgcn_readfirstlane(t.tn);
+    t.offA = __builtin_amdgcn_readfirstlane(t.offA);
+    t.offB = __builtin_amdgcn_readfirstlane(t.offB);
+    return t;
+}
+
+template <bool SUB>
+__global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArgs g) {
+    __shared__ __attribute__((aligned(1024))) int8_t smem[LDS_BYTES + PARK_SPARE];
+    static_assert(LDS_BYTES + PARK_SPARE <= 160 * 1024, "LDS");
+    static_assert(STAGES == 4 && GLDS_PER_STEP == 4 && PARK_STORES == 8, "vmcnt bookkeeping below assumes these");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    uint32_t *const spare = reinterpret_cast<uint32_t *>(smem + LDS_BYTES);
+
+    // this block's XCD queue: the XCD's share of every plane (the one-tile kernel's remap)
+    const unsigned G = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
+    const unsigned nblk = (G >> 3) + (xcd < (G & 7) ? 1u : 0u);  // blocks serving this queue
+    const unsigned P = g.mtiles * g.ntiles, q8 = P >> 3, r8 = P & 7;
+    const unsigned tx = q8 + (xcd < r8 ? 1u : 0u);
+    const unsigned basex = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+    const unsigned total = g.nplanes * tx;
+    auto tile_u = [&](unsigned i) {
+        const unsigned y = __builtin_amdgcn_readfirstlane(i / tx);
+        return y * P + basex + (i - y * tx);
+    };
+    auto claim = [&]() {  // raw queue position; the tile is (position + nblk) if below total
+        return __hip_atomic_fetch_add(g.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto to_tile = [&](unsigned pos) { return pos + nblk < total ? pos + nblk : NO_TILE; };
+    unsigned ccur = (bid >> 3) < total ? (bid >> 3) : NO_TILE;
+    if (ccur == NO_TILE) return;  // block-uniform, before any barrier
+    if (tid == 0) spare[0] = to_tile(claim());
+
+    const unsigned K = g.ksteps;  // >= 5 (host): the first two and the last three steps of a tile are apart
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
+    const uint32_t lds_wave = lds_base + wave * 1024;
+    const v4si rA = make_rsrc(g.A, g.regionA);
+    const v4si rB = make_rsrc(g.B, g.regionB);
+    const uint32_t lane_off = wave * 1024 + lane * 16;
+    auto lo_of = [&](unsigned step) { return lds_wave + (step & (STAGES - 1)) * SLOT; };
+    auto rd_of = [&](unsigned step) { return smem + (step & (STAGES - 1)) * SLOT; };
+
+    TileRef ct = decode_tile<SUB>(g, tile_u(ccur));
+    constexpr unsigned D = STAGES - 1;
+    for (unsigned s0 = 0; s0 < D; ++s0) {  // steps 0..2 of the first tile
+        const uint32_t lo = lo_of(s0);
+        bglds16(rA, ct.offA + s0 * PANEL + lane_off, lo);
+        bglds16(rA, ct.offA + s0 * PANEL + lane_off + 8192, lo + 8192);
+        bglds16(rB, ct.offB + s0 * PANEL + lane_off, lo + PANEL);
+        bglds16(rB, ct.offB + s0 * PANEL + lane_off + 8192, lo + PANEL + 8192);
+    }
+    wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();  // step 0 landed (and the claim's LDS write)
+    barrier();
+
+    unsigned s = 0;                                             // global k-step of this block (slot s mod 4)
+    unsigned cnext = __builtin_amdgcn_readfirstlane(spare[0]);  // the tile after the current one
+    uint32_t da = ct.offA + D * PANEL, db = ct.offB + D * PANEL;  // DMA cursor: panels of the next step staged
+    Frags f;
+    AccTile acc[ACC_I][ACC_J];
+    for (unsigned r = 0;; ++r) {
+        const int acc0 = g.biased ? g.bias[ct.j] : 0;
+#pragma unroll
+        for (int i = 0; i < ACC_I; ++i)
+#pragma unroll
+            for (int jj = 0; jj < ACC_J; ++jj) acc[i][jj] = AccTile{} + acc0;
+        if (wr == 1) barrier();  // group 1 falls one barrier behind (ping-pong, as in the one-tile kernel)
+        unsigned k = 0;
+        uint32_t na = 0, nb = 0;  // the next tile's step-0 panels
+        // one k-step: reads of slot s, DMA of step s+3 (this tile's step k+3, or the next tile's step
+        // k+3-K once k+3 >= K: the cursor jumps there after staging this tile's last step), wait, MFMAs
+        auto step = [&](auto wait) {
+            read_frags(f, rd_of(s), wr, wc, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t lo = lo_of(s + D);
+            bglds16(rA, da + lane_off, lo);
+            bglds16(rA, da + lane_off + 8192, lo + 8192);
+            bglds16(rB, db + lane_off, lo + PANEL);
+            bglds16(rB, db + lane_off + 8192, lo + PANEL + 8192);
+            const bool jump = k + D + 1 == K;
+            da = jump ? na : da + PANEL;
+            db = jump ? nb : db + PANEL;
+            wait();
+            barrier();
+            mfma_step(acc, f);
+            barrier();
+        };
+        if (r > 0) {
+            // steps 0 and 1: the previous tile's 8 residue stores are younger than the awaited DMA
+            for (; k < 2; ++k, ++s) step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1) + PARK_STORES>(); });
+            cnext = __builtin_amdgcn_readfirstlane(spare[0]);  // written by wave 0 two barriers ago
+        }
+        TileRef nt = ct;
+        if (cnext != NO_TILE) {
+            nt = decode_tile<SUB>(g, tile_u(cnext));
+            na = nt.offA;
+            nb = nt.offB;
+        }
+        // steady steps; the block's last tile stops staging three steps before its end
+        const unsigned kend = cnext != NO_TILE ? K : K - D;
+        for (; k < kend; ++k, ++s) step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>(); });
+        for (; k < K; ++k, ++s) {  // drain of the block's last tile
+            read_frags(f, rd_of(s), wr, wc, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            wait_steps_lgkm0<GLDS_PER_STEP>(k + 2 < K ? (int)(K - k - 2) : 0);  // steps k+2..K-1 may fly
+            barrier();
+            mfma_step(acc, f);
+            barrier();
+        }
+        if (wr == 0) barrier();  // realign the groups
+        barrier();
+
+        // epilogue: the tile after next is claimed first (its latency hides under the residue
+        // arithmetic), residues -> LDS (columns 0..127 in the slot of the tile's last step, 128..255
+        // in the spare), then 16-byte column stores; the ring slot is reused by the DMA of step
+        // s+3, issued after the closing barrier
+        unsigned pos = 0;
+        const bool claiming = tid == 0 && cnext != NO_TILE;
+        if (claiming) pos = claim();
+        // per-thread epilogue addresses derive from this copy of the thread index, opaque to the
+        // compiler, so they are recomputed per tile instead of hoisted out of the tile loop (held
+        // across the main loop they spilled, and the spill reloads' vmcnt waits then serialised the
+        // residue stores)
+        int etid = tid;
+        asm volatile("" : "+v"(etid));
+        const int elane = etid & 63;
+        const int p = g.p[ct.j];
+        uint32_t *parkA = reinterpret_cast<uint32_t *>(rd_of(s - 1));
+        uint32_t *parkB = spare;
+        uint32_t *lo = wc < 2 ? parkA : parkB;  // this wave's 64 columns lie in one half
+        auto park = [&](auto &&res) {
+#pragma unroll
+            for (int i = 0; i < ACC_I; ++i)
+#pragma unroll
+                for (int jj = 0; jj < ACC_J; ++jj) {
+                    const int col = wc * 64 + acc_col(jj, elane);
+#pragma unroll
+                    for (int gq = 0; gq < ACC_E / 4; ++gq) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][4 * gq + e]) << (8 * e);
+                        const int rdw = (wr * 128 + acc_row(i, 4 * gq, elane)) >> 2;
+                        lo[(col & 127) * 64 + (rdw ^ (col & 31))] = w;
+                    }
+                }
+        };
+        if (g.biased) {
+            const uint32_t m = g.minv[ct.j];
+            park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
+        } else {
+            const int bar = g.barrett[ct.j];
+            const bool p256 = (p == 256);
+            park([&](int x) { return residue(x, p, bar, p256); });
+        }
+        __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0), vmcnt untouched
+        barrier();
+        uint8_t *out = static_cast<uint8_t *>(g.out) + ct.j * g.planeOut + ct.sb * g.subOut +
+                       (size_t)ct.tn * 256 * g.ldo + (size_t)ct.tm * 256;
+#pragma unroll
+        for (int it = 0; it < PARK_STORES; ++it) {
+            const int chunk = etid + NTHREADS * it;
+            const int col = chunk >> 4, qd = chunk & 15;
+            const int x = col & 31;
+            const uint32_t *src = it < PARK_STORES / 2 ? parkA : parkB;
+            const uint4 v = *reinterpret_cast<const uint4 *>(src + (col & 127) * 64 + ((4 * qd) ^ (x & ~3)));
+            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+            const int pm = x & 3;
+            *reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd) =
+                make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+        }
+        __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // park reads done
+        barrier();
+        if (tid == 0) spare[0] = claiming ? to_tile(pos) : NO_TILE;  // read at the next tile's k = 1
+        if (cnext == NO_TILE) break;
+        ct = nt;
+    }
+}
 
 // Exhaustive check of the two residue epilogues against exact arithmetic, every input and every
 // modulus: path 0 = biased (x in [-2^30, 2^30], the accumulator starting at bias_i), path 1 = signed
@@ -551,8 +790,32 @@ unsigned long long residue_selftest(int path, hipStream_t st) {
     return h;
 }
 
+// CUs of the current device (one persistent block each)
+static unsigned device_cu_count() {
+    static unsigned cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cached[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cached[dev] = (unsigned)n;
+    }
+    return cached[dev];
+}
+// GEMMUL8_PERSISTENT: 0 = one-tile kernel only, 1 = persistent kernel wherever it applies, unset =
+// persistent when the launch has at least four tiles per CU.  g_persistent_override (probes) wins when >= 0.
+int g_persistent_override = -1;
+static int persistent_mode() {
+    if (g_persistent_override >= 0) return g_persistent_override;
+    static const int env = [] {
+        const char *e = getenv("GEMMUL8_PERSISTENT");
+        return e ? atoi(e) : 2;
+    }();
+    return env;
+}
+
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
-             int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st) {
+             int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue) {
     GemmArgs g{};
     g.A = A8;
     g.B = B8;
@@ -605,6 +868,32 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
             if (k0 == 0) buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0);
             else buf ? OZ2_GEMM(EPI_RESIDUE_ADD, 1) : OZ2_GEMM(EPI_RESIDUE_ADD, 0);
         }
+        return;
+    }
+    // persistent residue kernel: a tile-queue area, whole-region buffer descriptors (< 4 GiB),
+    // >= 5 k-steps per tile (the stores' two steps and the DMA's last three steps of a tile are
+    // apart) and, by default, >= 4 tiles per CU (measured, same process: cfg2 products 5.16 -> 5.04 ms,
+    // 8192^2 x 1024 1.14 -> 1.01 ms, 4096^3 0.857 -> 0.842 ms; at 2048^3, 3.5 tiles per CU, the
+    // queue-zeroing launch costs more than the persistent kernel saves: 0.115 -> 0.118 ms)
+    const unsigned ntiles_all = (unsigned)(L.mtiles * L.ntiles) * nplanes * g.nsub;
+    const size_t regA = (size_t)nplanes * L.planeA, regB = (size_t)nplanes * L.planeB;
+    const unsigned ncu = device_cu_count();
+    const int pmode = persistent_mode();
+    if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && regA < ((size_t)1 << 32) &&
+        regB < ((size_t)1 << 32) && g.ksteps >= 5 && (pmode == 1 || ntiles_all >= 4 * ncu)) {
+        g.nplanes = nplanes * g.nsub;
+        g.regionA = (uint32_t)regA;
+        g.regionB = (uint32_t)regB;
+        g.queue = queue;
+        zero_i32(reinterpret_cast<int32_t *>(queue), 8, st);
+        // GEMMUL8_PERSISTENT_GRID caps the grid (tests: many tiles per block at small shapes)
+        static const unsigned grid_cap = [] {
+            const char *e = getenv("GEMMUL8_PERSISTENT_GRID");
+            return e ? (unsigned)atoi(e) : 0u;
+        }();
+        const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 1u) : ncu));
+        if (g.nsub == 3) gemm_i8_persistent_kernel<true><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        else gemm_i8_persistent_kernel<false><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         return;
     }
     switch (epi) {

@@ -196,6 +196,7 @@ struct Views {
     uint8_t *R;
     int16_t *sftA, *sftB, *sft0;
     int32_t *bound;
+    uint32_t *queue;
 };
 static Views views(void *work, size_t m, size_t n, size_t k, unsigned N, bool cplx, unsigned slice_planes = 0) {
     Views v;
@@ -208,6 +209,7 @@ static Views views(void *work, size_t m, size_t n, size_t k, unsigned N, bool cp
     v.sftB = reinterpret_cast<int16_t *>(base + v.L.offSftB);
     v.bound = reinterpret_cast<int32_t *>(base + v.L.offBound);
     v.sft0 = reinterpret_cast<int16_t *>(base + v.L.offSft0);
+    v.queue = reinterpret_cast<uint32_t *>(base + v.L.offQueue);
     return v;
 }
 
@@ -302,7 +304,7 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
 static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1, unsigned slot, hipStream_t st) {
     const Layout &L = v.L;
     gemm_i8(v.A8 + slot * L.planeA, v.B8 + slot * L.planeB, L, j1 - j0, Epi::RESIDUE, v.R + j0 * L.planeR, nullptr,
-            nullptr, sub_mod_params(N, j0, j1), st);
+            nullptr, sub_mod_params(N, j0, j1), st, v.queue);
 }
 
 // phase 3: CRT + scaling + BLAS epilogue over all N residue planes

@@ -61,7 +61,7 @@ struct Layout {
     size_t bm_pad, bn_pad;
     unsigned S;                    // slice planes held at once (= N unless low-memory mode)
     // workspace offsets (bytes)
-    size_t offA, offB, offR, offSftA, offSftB, offBound, offSft0, total;
+    size_t offA, offB, offR, offSftA, offSftB, offBound, offSft0, offQueue, total;
 };
 
 static inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -139,6 +139,7 @@ static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool 
     L.offSftB = off; off += round_up(L.bn_pad * 2, 256);
     L.offBound = off; off += round_up((L.bm_pad + L.bn_pad) * 4, 256);
     L.offSft0 = off; off += round_up((L.bm_pad + L.bn_pad) * 2, 256);
+    L.offQueue = off; off += 256;  // 8 per-XCD tile-queue heads of the persistent product kernel
     L.total = off;
     return L;
 }

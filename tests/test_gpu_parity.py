@@ -566,3 +566,38 @@ def test_stale_hip_error_is_not_reported():
     torch.cuda.synchronize()
     assert hip.hipPeekAtLastError() == 0
     assert bits_equal(np.asfortranarray(dC.cpu().numpy().T), Co)
+
+
+def test_persistent_products_forced():
+    """GEMMUL8_PERSISTENT=1 (child process): the persistent residue kernel (per-XCD tile queues,
+    k-step pipeline across tiles, residue stores in flight under the next tile) at small shapes,
+    also with the grid capped to 16 blocks (GEMMUL8_PERSISTENT_GRID) so every block walks many
+    tiles and the queues of four XCDs stay empty; slices, residues and C against the oracle for
+    real f64 / f32, accurate mode, the signed residue path (k_pad > 2^16), Karatsuba complex
+    sub-products, and low-memory mode (several product launches on one workspace); the workspace
+    starts as 0xA5 bytes, so the queue heads are garbage until the launch zeroes them"""
+    import subprocess
+    code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
+            "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
+            "import gemmul8 as G, torch\n"
+            "rng = np.random.default_rng(23)\n"
+            "check_full(randmat_np(rng, 300, 513), randmat_np(rng, 513, 260), 14)\n"
+            "check_full(randmat_np(rng, 700, 333), randmat_np(rng, 333, 530), 9, fast=False)\n"
+            "check_full(randmat_np(rng, 520, 400, dtype=np.float32), randmat_np(rng, 400, 270, dtype=np.float32), 7)\n"
+            "check_full(randmat_np(rng, 20, 70000), randmat_np(rng, 70000, 24), 14)\n"
+            "check_full(randmat_np(rng, 300, 333, dtype=np.complex128), randmat_np(rng, 333, 290, dtype=np.complex128), 12, ctype=3)\n"
+            "m, n, k, N = 600, 520, 700, 14\n"
+            "A = torch.randn((k, m), dtype=torch.float64, device='cuda'); B = torch.randn((n, k), dtype=torch.float64, device='cuda')\n"
+            "Cs = []\n"
+            "for S in (None, 3):\n"
+            "    W = G.alloc_work(m, n, k, N, 0, slice_planes=S); W.fill_(0xA5); C = torch.empty((n, m), dtype=torch.float64, device='cuda')\n"
+            "    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, True, W, 0, slice_planes=S); Cs.append(C.cpu())\n"
+            "assert torch.equal(Cs[0], Cs[1])\n"
+            "print('OK')")
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    for cap in ("", "16"):
+        env = dict(os.environ, GEMMUL8_PERSISTENT="1", GEMMUL8_PERSISTENT_GRID=cap, GEMMUL8_CPLX_PRODUCTS="karatsuba")
+        r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "OK" in r.stdout, (cap, r.stderr[-3000:])
