@@ -32,7 +32,7 @@ __device__ __forceinline__ int center_sum(int a, int b, int p) {
     return s;
 }
 #ifndef OZ2_ENC_ABLATE
-#define OZ2_ENC_ABLATE 0  // probe builds only (tools/probes/enc_probe.hip)
+#define OZ2_ENC_ABLATE 0  // probe builds only (tools/probes/enc_probe.hip, fused_probe.hip)
 #endif
 
 // f64 residues in groups of moduli.  mod_8i (scaling.hpp:215-223) reduces the integer-valued x
@@ -338,93 +338,25 @@ __global__ __launch_bounds__(256) void stats_pair_kernel(const double *__restric
 // stores the last k mod 4 imaginary magnitudes outside the column, leaving them 0 in
 // the bound product -- extract_B8i_kernel_bigmatrix, scaling.hpp:2313-2321).
 // ------------------------------------------------------------------
-template <typename R, bool CPLX> using EncTile = R[CPLX ? 32 : 64][64 + 1][CPLX ? 2 : 1];
-
-template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
-__device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
-                                            const int16_t *__restrict__ sft, int8_t *__restrict__ out, size_t plane,
-                                            size_t ksteps, size_t kblk, size_t vmax, int flags, const ModParams &MP,
-                                            const ModGroups &G, unsigned bx, unsigned by, EncTile<R, CPLX> &tile) {
-    constexpr int KT = CPLX ? 32 : 64;
-    constexpr int NT = CPLX ? 128 : 256;
-    constexpr int NC = CPLX ? 2 : 1;
-    // contiguous vectors: blockIdx.x walks k so that co-running blocks read neighbouring 512-B
-    // pieces of the same vectors (walking the vectors instead puts every co-running block at
-    // the same offset modulo the vector stride, i.e. on the same HBM channels)
-    const bool kfirst = CONTIG && (flags & ENC_KFIRST);
-    const size_t v0 = (size_t)(kfirst ? by : bx) * 64;
-    const size_t e0 = (size_t)(kfirst ? bx : by) * KT;
-    const int tid = threadIdx.x;
-
-    // stage the tile, coalesced along whichever index is contiguous in HBM; interior tiles
-    // load without per-element guards so all loads are in flight at once
-    constexpr int NL = (64 * KT) / NT;
-    const bool interior = v0 + 64 <= nvec && e0 + KT <= len;
-    R lre[NL], lim[NL];
-    if (OZ2_ENC_ABLATE == 2) {  // probe builds only: no loads
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            lre[i] = (R)(tid * 37 + i * 1.25 + v0);
-            lim[i] = 0;
-        }
-    } else if (interior) {  // block-uniform branch: one batch of unguarded loads
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            const int idx = tid + NT * i;
-            int vl, el;
-            if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
-            const size_t v = v0 + vl, e = e0 + el;
-            load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-            const int idx = tid + NT * i;
-            int vl, el;
-            if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
-            const size_t v = v0 + vl, e = e0 + el;
-            lre[i] = 0;
-            lim[i] = 0;
-            if (v < nvec && e < len) load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < NL; ++i) {
-        const int idx = tid + NT * i;
-        int vl, el;
-        if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
-        tile[el][vl][0] = lre[i];
-        if (CPLX) tile[el][vl][NC - 1] = (flags & ENC_CONJ) ? -lim[i] : lim[i];
-    }
-    __syncthreads();
-
-    const int vl = tid & 63, c = tid >> 6;  // c-th 16-element chunk of the tile
-    const size_t v = v0 + vl;
-    const size_t kk = e0 + 16 * c;
-    int s = 0;
-    if (v < nvec) s = MODE == 0 ? -(int)sft[v] : (int)sft[v];
-
-    R yr[16], yi[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        R re = tile[16 * c + q][vl][0];
-        R im = CPLX ? tile[16 * c + q][vl][NC - 1] : R(0);
-        if (MODE == 0) {
-            yr[q] = trunc(scalbn(re, s));
-            yi[q] = trunc(scalbn(im, s));
-        } else {
-            yr[q] = scalbn(fabs(re), s);
-            yi[q] = scalbn(fabs(im), s);
-        }
-    }
-
+// The N slices (MODE 0) or the magnitude plane (MODE 1) of 16 consecutive elements kk..kk+15 of
+// vector v, already scaled (yr, yi = trunc(x * 2^sft) resp. |x| * 2^sft0), into the panel layout.
+template <typename R, bool CPLX, bool IS_A, int MODE>
+__device__ __forceinline__ void encode_vec16(const R (&yr)[16], const R (&yi)[16], size_t v, size_t kk, size_t nvec,
+                                             size_t len, int8_t *__restrict__ out, size_t plane, size_t ksteps,
+                                             size_t kblk, size_t vmax, int flags, const ModParams &MP,
+                                             const ModGroups &G) {
     const bool top = v < nvec || !CPLX || !IS_A;  // complex A: rows >= m only emit their (zero) bottom copy
     const bool kara = CPLX && (flags & ENC_KARA) != 0;
     // one plane of slices: real -> (v, kk); complex A -> [wr, -wi] / [wi, wr]; complex B -> [wr; wi];
     // Karatsuba (either operand): vectors v, v + vmax, v + 2 vmax <- wr, wi, ws = (wr + wi) mod p
     auto emit = [&](int8_t *o, const uint32_t (&wr)[4], const uint32_t (&wi)[4], const uint32_t (&ws)[4]) {
         if (!CPLX) {
-            *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+            if (OZ2_ENC_ABLATE == 3)  // probe builds only: vector-major slices (each vector's bytes contiguous)
+                *reinterpret_cast<uint4 *>(o + v * ksteps * KSTEP + kk) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
+            else if (OZ2_ENC_ABLATE == 4)  // probe builds only: no slice stores
+                asm volatile("" ::"v"(wr[0]), "v"(wr[1]), "v"(wr[2]), "v"(wr[3]));
+            else
+                *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
         } else if (kara) {
             *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
             *reinterpret_cast<uint4 *>(o + panel_offset(v + vmax, kk, ksteps)) = make_uint4(wi[0], wi[1], wi[2], wi[3]);
@@ -666,6 +598,89 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
             emit(out + (size_t)j * plane, wr, wi, ws);
         }
     }
+}
+
+template <typename R, bool CPLX> using EncTile = R[CPLX ? 32 : 64][64 + 1][CPLX ? 2 : 1];
+
+template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
+__device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                            const int16_t *__restrict__ sft, int8_t *__restrict__ out, size_t plane,
+                                            size_t ksteps, size_t kblk, size_t vmax, int flags, const ModParams &MP,
+                                            const ModGroups &G, unsigned bx, unsigned by, EncTile<R, CPLX> &tile) {
+    constexpr int KT = CPLX ? 32 : 64;
+    constexpr int NT = CPLX ? 128 : 256;
+    constexpr int NC = CPLX ? 2 : 1;
+    // contiguous vectors: blockIdx.x walks k so that co-running blocks read neighbouring 512-B
+    // pieces of the same vectors (walking the vectors instead puts every co-running block at
+    // the same offset modulo the vector stride, i.e. on the same HBM channels)
+    const bool kfirst = CONTIG && (flags & ENC_KFIRST);
+    const size_t v0 = (size_t)(kfirst ? by : bx) * 64;
+    const size_t e0 = (size_t)(kfirst ? bx : by) * KT;
+    const int tid = threadIdx.x;
+
+    // stage the tile, coalesced along whichever index is contiguous in HBM; interior tiles
+    // load without per-element guards so all loads are in flight at once
+    constexpr int NL = (64 * KT) / NT;
+    const bool interior = v0 + 64 <= nvec && e0 + KT <= len;
+    R lre[NL], lim[NL];
+    if (OZ2_ENC_ABLATE == 2) {  // probe builds only: no loads
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            lre[i] = (R)(tid * 37 + i * 1.25 + v0);
+            lim[i] = 0;
+        }
+    } else if (interior) {  // block-uniform branch: one batch of unguarded loads
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            const int idx = tid + NT * i;
+            int vl, el;
+            if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
+            const size_t v = v0 + vl, e = e0 + el;
+            load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+            const int idx = tid + NT * i;
+            int vl, el;
+            if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
+            const size_t v = v0 + vl, e = e0 + el;
+            lre[i] = 0;
+            lim[i] = 0;
+            if (v < nvec && e < len) load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const int idx = tid + NT * i;
+        int vl, el;
+        if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
+        tile[el][vl][0] = lre[i];
+        if (CPLX) tile[el][vl][NC - 1] = (flags & ENC_CONJ) ? -lim[i] : lim[i];
+    }
+    __syncthreads();
+
+    const int vl = tid & 63, c = tid >> 6;  // c-th 16-element chunk of the tile
+    const size_t v = v0 + vl;
+    const size_t kk = e0 + 16 * c;
+    int s = 0;
+    if (v < nvec) s = MODE == 0 ? -(int)sft[v] : (int)sft[v];
+
+    R yr[16], yi[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        R re = tile[16 * c + q][vl][0];
+        R im = CPLX ? tile[16 * c + q][vl][NC - 1] : R(0);
+        if (MODE == 0) {
+            yr[q] = trunc(scalbn(re, s));
+            yi[q] = trunc(scalbn(im, s));
+        } else {
+            yr[q] = scalbn(fabs(re), s);
+            yi[q] = scalbn(fabs(im), s);
+        }
+    }
+
+    encode_vec16<R, CPLX, IS_A, MODE>(yr, yi, v, kk, nvec, len, out, plane, ksteps, kblk, vmax, flags, MP, G);
 }
 
 template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
