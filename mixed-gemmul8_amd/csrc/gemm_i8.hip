@@ -209,8 +209,11 @@ __device__ __forceinline__ void read_frags(Frags &f, const int8_t *slot, int wr,
 #ifndef OZ2_MFMA_ORDER
 #define OZ2_MFMA_ORDER 0  // probe builds: 0 = A-major (4 consecutive MFMAs share an A fragment), 1 = B-major
 #endif
+// PRIO 0: the MFMA interval runs at priority 1 (raised and dropped around every interval); other
+// values leave the wave's priority alone (the persistent kernel's static-priority variants)
+template <int PRIO = 0>
 __device__ __forceinline__ void mfma_step(AccTile (&acc)[ACC_I][ACC_J], const Frags &f) {
-    __builtin_amdgcn_s_setprio(1);
+    if (PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int x = 0; x < 32; ++x) {
         const int i = OZ2_MFMA_ORDER ? (x & 7) : (x >> 2), jj = OZ2_MFMA_ORDER ? (x >> 3) : (x & 3);
@@ -220,7 +223,7 @@ __device__ __forceinline__ void mfma_step(AccTile (&acc)[ACC_I][ACC_J], const Fr
             acc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[i], f.b[jj], acc[i][jj], 0, 0, 0);
         }
     }
-    __builtin_amdgcn_s_setprio(0);
+    if (PRIO == 0) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
 }
 // accumulator map (16x16 tiles): col = lane & 15, row = 4 (lane >> 4) + e, e = 0..3
@@ -257,8 +260,9 @@ __device__ __forceinline__ void read_frags(Frags &f, const int8_t *slot, int wr,
     }
 }
 
+template <int PRIO = 0>
 __device__ __forceinline__ void mfma_step(AccTile (&acc)[ACC_I][ACC_J], const Frags &f) {
-    __builtin_amdgcn_s_setprio(1);
+    if (PRIO == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -271,7 +275,7 @@ __device__ __forceinline__ void mfma_step(AccTile (&acc)[ACC_I][ACC_J], const Fr
                 acc[i][jj] = __builtin_amdgcn_mfma_i32_32x32x32_i8(f.a[s][i], f.b[s][jj], acc[i][jj], 0, 0, 0);
             }
         }
-    __builtin_amdgcn_s_setprio(0);
+    if (PRIO == 0) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -564,7 +568,12 @@ template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArg
     return t;
 }
 
-template <bool SUB>
+// PRIO: 1 (default) = static priority 1 for waves 4-7, the younger half (one barrier behind), which
+// otherwise loses every issue arbitration to its older partner (MI355X_MICROARCH.md, two waves per
+// SIMD, item 4); 0 = priority 1 around every MFMA interval (as the one-tile kernel); 2 = no priority
+// changes.  Measured in one process (tools/probes/persist_prio.hip, random bytes): 1 and 2 are
+// 0.3-0.8 % faster than 0 at 8192^3, 4096^3 and 8192^2 x 1024, with identical residues.
+template <bool SUB, int PRIO = 1>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(1024))) int8_t smem[LDS_BYTES + PARK_SPARE];
     static_assert(LDS_BYTES + PARK_SPARE <= 160 * 1024, "LDS");
@@ -573,6 +582,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
     uint32_t *const spare = reinterpret_cast<uint32_t *>(smem + LDS_BYTES);
+    if (PRIO == 1 && wr == 1) __builtin_amdgcn_s_setprio(1);
 
     // this block's XCD queue: the XCD's share of every plane (the one-tile kernel's remap)
     const unsigned G = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
@@ -643,7 +653,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             db = jump ? nb : db + PANEL;
             wait();
             barrier();
-            mfma_step(acc, f);
+            mfma_step<PRIO>(acc, f);
             barrier();
         };
         if (r > 0) {
@@ -665,7 +675,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             __builtin_amdgcn_sched_barrier(0);
             wait_steps_lgkm0<GLDS_PER_STEP>(k + 2 < K ? (int)(K - k - 2) : 0);  // steps k+2..K-1 may fly
             barrier();
-            mfma_step(acc, f);
+            mfma_step<PRIO>(acc, f);
             barrier();
         }
         if (wr == 0) barrier();  // realign the groups
@@ -805,6 +815,7 @@ static unsigned device_cu_count() {
 // GEMMUL8_PERSISTENT: 0 = one-tile kernel only, 1 = persistent kernel wherever it applies, unset =
 // persistent when the launch has at least four tiles per CU.  g_persistent_override (probes) wins when >= 0.
 int g_persistent_override = -1;
+int g_prio_override = 1;  // probes: the persistent kernel's priority variant (PRIO; 1 = the default)
 static int persistent_mode() {
     if (g_persistent_override >= 0) return g_persistent_override;
     static const int env = [] {
@@ -892,8 +903,10 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
             return e ? (unsigned)atoi(e) : 0u;
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 1u) : ncu));
-        if (g.nsub == 3) gemm_i8_persistent_kernel<true><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else gemm_i8_persistent_kernel<false><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        if (g.nsub == 3) gemm_i8_persistent_kernel<true, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        else if (g_prio_override == 0) gemm_i8_persistent_kernel<false, 0><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        else if (g_prio_override == 2) gemm_i8_persistent_kernel<false, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        else gemm_i8_persistent_kernel<false, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         return;
     }
     switch (epi) {
