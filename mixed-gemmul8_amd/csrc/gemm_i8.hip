@@ -603,7 +603,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
     if (ccur == NO_TILE) return;  // block-uniform, before any barrier
     if (tid == 0) spare[0] = to_tile(claim());
 
-    const unsigned K = g.ksteps;  // >= 5 (host): the first two and the last three steps of a tile are apart
+    // K >= 6 (host): the DMA cursor jumps to the next tile after staging this tile's last step, at
+    // k = K - 4, which must come after steps 0 and 1, where a block's later tiles learn their successor
+    // (with K = 5 the jump read the successor's offsets before they were decoded)
+    const unsigned K = g.ksteps;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
     const uint32_t lds_wave = lds_base + wave * 1024;
     const v4si rA = make_rsrc(g.A, g.regionA);
@@ -882,8 +885,7 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         return;
     }
     // persistent residue kernel: a tile-queue area, whole-region buffer descriptors (< 4 GiB),
-    // >= 5 k-steps per tile (the stores' two steps and the DMA's last three steps of a tile are
-    // apart) and, by default, >= 4 tiles per CU (measured, same process: cfg2 products 5.16 -> 5.04 ms,
+    // >= 6 k-steps per tile (the kernel's cursor jump at k = K - 4 after its first two steps) and, by default, >= 4 tiles per CU (measured, same process: cfg2 products 5.16 -> 5.04 ms,
     // 8192^2 x 1024 1.14 -> 1.01 ms, 4096^3 0.857 -> 0.842 ms; at 2048^3, 3.5 tiles per CU, the
     // queue-zeroing launch costs more than the persistent kernel saves: 0.115 -> 0.118 ms)
     const unsigned ntiles_all = (unsigned)(L.mtiles * L.ntiles) * nplanes * g.nsub;
@@ -891,7 +893,7 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     const unsigned ncu = device_cu_count();
     const int pmode = persistent_mode();
     if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && regA < ((size_t)1 << 32) &&
-        regB < ((size_t)1 << 32) && g.ksteps >= 5 && (pmode == 1 || ntiles_all >= 4 * ncu)) {
+        regB < ((size_t)1 << 32) && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 4 * ncu)) {
         g.nplanes = nplanes * g.nsub;
         g.regionA = (uint32_t)regA;
         g.regionB = (uint32_t)regB;

@@ -582,6 +582,8 @@ def test_persistent_products_forced():
             "import gemmul8 as G, torch\n"
             "rng = np.random.default_rng(23)\n"
             "check_full(randmat_np(rng, 300, 513), randmat_np(rng, 513, 260), 14)\n"
+            "check_full(randmat_np(rng, 300, 300), randmat_np(rng, 300, 260), 14)\n"  # 5 k-steps per tile
+            "check_full(randmat_np(rng, 300, 330), randmat_np(rng, 330, 260), 14)\n"  # 6 k-steps per tile
             "check_full(randmat_np(rng, 700, 333), randmat_np(rng, 333, 530), 9, fast=False)\n"
             "check_full(randmat_np(rng, 520, 400, dtype=np.float32), randmat_np(rng, 400, 270, dtype=np.float32), 7)\n"
             "check_full(randmat_np(rng, 20, 70000), randmat_np(rng, 70000, 24), 14)\n"
@@ -601,3 +603,39 @@ def test_persistent_products_forced():
         r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0 and "OK" in r.stdout, (cap, r.stderr[-3000:])
+
+
+def test_persistent_default_matches_one_tile():
+    """Production shapes where the default rule picks the persistent residue kernel (>= 4 tiles per
+    CU): C bit-identical to the one-tile kernel (GEMMUL8_PERSISTENT=0, child process) at k-steps per
+    tile around the kernel's minimum (5: one-tile kernel; 6, 7, 128: persistent).  With 5 k-steps
+    the persistent kernel's DMA cursor used to jump to the next tile before it was decoded."""
+    import subprocess
+    import tempfile
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    code = ("import sys, numpy as np, torch; sys.path[:0] = sys.argv[1:3]\n"
+            "import gemmul8 as G\n"
+            "out = sys.argv[3]; res = {}\n"
+            "for k in (300, 330, 400, 8192):\n"
+            "    m = n = 4096\n"
+            "    g = torch.Generator(device='cuda'); g.manual_seed(k)\n"
+            "    A = torch.randn((k, m), dtype=torch.float64, device='cuda', generator=g)\n"
+            "    B = torch.randn((n, k), dtype=torch.float64, device='cuda', generator=g)\n"
+            "    C = torch.empty((n, m), dtype=torch.float64, device='cuda')\n"
+            "    W = G.alloc_work(m, n, k, 14)\n"
+            "    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C, m, 14, True, W)\n"
+            "    res[str(k)] = C.cpu().numpy()\n"
+            "np.savez(out, **res)\n")
+    with tempfile.TemporaryDirectory() as d:
+        outs = []
+        for mode in ("0", ""):
+            out = os.path.join(d, f"c{mode or 'default'}.npz")
+            env = dict(os.environ, GEMMUL8_PERSISTENT=mode) if mode else {
+                kk: v for kk, v in os.environ.items() if kk != "GEMMUL8_PERSISTENT"}
+            r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "mixed-gemmul8_amd"), tdir, out],
+                               env=env, capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0, r.stderr[-3000:]
+            outs.append(np.load(out))
+        for k in outs[0].files:
+            assert np.array_equal(outs[0][k].view(np.uint64), outs[1][k].view(np.uint64)), k
