@@ -899,12 +899,13 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         g.regionB = (uint32_t)regB;
         g.queue = queue;
         zero_i32(reinterpret_cast<int32_t *>(queue), 8, st);
-        // GEMMUL8_PERSISTENT_GRID caps the grid (tests: many tiles per block at small shapes)
+        // GEMMUL8_PERSISTENT_GRID caps the grid (tests: many tiles per block at small shapes), at no fewer
+        // than 8 blocks: every XCD queue that holds tiles needs a block of its own (bid mod 8)
         static const unsigned grid_cap = [] {
             const char *e = getenv("GEMMUL8_PERSISTENT_GRID");
             return e ? (unsigned)atoi(e) : 0u;
         }();
-        const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 1u) : ncu));
+        const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
         if (g.nsub == 3) gemm_i8_persistent_kernel<true, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else if (g_prio_override == 0) gemm_i8_persistent_kernel<false, 0><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else if (g_prio_override == 2) gemm_i8_persistent_kernel<false, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);

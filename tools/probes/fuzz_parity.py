@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Randomised parity sweep (GPU vs CPU oracle, bit-exact via tests/test_gpu_parity.check_full):
-random shapes, moduli counts, modes, type combinations and ops.  python fuzz_parity.py [cases] [seed]"""
+random shapes, moduli counts, modes, type combinations and ops.  python fuzz_parity.py [cases] [seed]
+(GEMMUL8_PERSISTENT=1 GEMMUL8_PERSISTENT_GRID=16 puts every residue product on the persistent kernel
+with many tiles per block)"""
 import sys
 import time
 
@@ -35,5 +37,7 @@ for c in range(cases):
     except AssertionError as e:
         fails += 1
         print("FAIL", desc, str(e)[:200], flush=True)
+    if (c + 1) % 50 == 0:
+        print(f"{c + 1} cases, {fails} failures, {time.time() - t0:.0f} s", flush=True)
 print(f"{cases} cases, {fails} failures, {time.time() - t0:.0f} s", flush=True)
 sys.exit(1 if fails else 0)
