@@ -105,9 +105,10 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
                            void *work, int32_t *C32);
 
 /* Validation hook: exhaustive exactness check of the product kernel's residue epilogue against exact
- * arithmetic, for all 20 moduli -- path 0: the biased reduction over every x in [-2^30, 2^30];
- * path 1: the reference's signed Barrett step (conv_32i_2_8u.hpp:7-56) over every int32.  Returns the
- * number of mismatching (input, modulus) pairs (0 expected; path 2 is a negative control that compares path 0
+ * arithmetic, for all 20 moduli -- path 0: the biased reduction (integer Barrett) over every x in
+ * [-2^30, 2^30]; path 3: the same range through the f64 form the product kernels use; path 1: the
+ * reference's signed Barrett step (conv_32i_2_8u.hpp:7-56) over every int32.  Returns the number of
+ * mismatching (input, modulus) pairs (0 expected; path 2 is a negative control that compares path 0
  * with a wrong expectation, so every pair mismatches). */
 unsigned long long gemmul8_residue_selftest(void *stream, int path);
 

@@ -71,6 +71,7 @@ struct GemmArgs {
     int barrett[OZ2_MAX_MODULI];     // floor(2^32/p) - 1 (signed path, reference conv_32i_2_8u)
     uint32_t minv[OZ2_MAX_MODULI];   // floor(2^32/p)     (biased unsigned path)
     int bias[OZ2_MAX_MODULI];        // ceil(2^30/p) * p  (accumulator start value, biased path)
+    double invp[OZ2_MAX_MODULI];     // fl(1/p)           (f64 form of the biased path)
     int biased;                      // |product| <= 2^30 (k_pad <= 2^16): biased path
     // sub-products per modulus (Karatsuba complex: 3, blockIdx.y = 3 j + s), each offset by s times
     // these strides in the A, B and output planes
@@ -163,6 +164,19 @@ __device__ __forceinline__ uint32_t residue_biased(uint32_t u, uint32_t p, uint3
     const uint32_t q = __umulhi(u, m);
     const uint32_t r = u - __umul24(q, p);
     return min(r, r - p);
+}
+
+// The same residue in f64 (p < 256; the product epilogues' form): zc = 2^52 + u exactly (the bit
+// pattern 0x43300000:u), so fma(zc, fl(1/p), -2^52 fl(1/p) + 2^-8) = u fl(1/p) + 2^-8 (the constant
+// is exact: 2^52 fl(1/p) is a multiple of 2^-8; the fma's rounding and fl(1/p)'s error stay below
+// 2^-28 for u < 2^32), whose floor is floor(u/p) because 0 < r/p + 2^-8 < 1 for every r <= p - 1 < 255;
+// then fma(q, -p, zc) = 2^52 + r exactly and the low dword of that double is r.  Three f64 ops, no
+// 32-bit integer multiply.  For p = 256 the epilogues take the low byte of u (the bias is a multiple
+// of 256).  gemmul8_residue_selftest path 3 checks it for every u of the biased range.
+__device__ __forceinline__ uint32_t residue_biased_f64(uint32_t u, double invp, double cneg, double pneg) {
+    const double zc = __hiloint2double(0x43300000, (int)u);
+    const double q = __builtin_floor(__builtin_fma(zc, invp, cneg));
+    return (uint32_t)__double2loint(__builtin_fma(q, pneg, zc));
 }
 
 // four residues in [0, p) per word: (a + b) mod p bytewise
@@ -312,11 +326,12 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I
                     __builtin_amdgcn_sched_barrier(0);
                 }
         };
-        if (OZ2_ABLATE == 7) {  // probe: the low byte only (cost of the mod-p reduction)
+        if (OZ2_ABLATE == 7 || (g.biased && p == 256)) {  // (7: probe) p = 256: bias is a multiple of 256
             park([&](int x) { return (uint32_t)x & 0xffu; });
         } else if (g.biased) {
-            const uint32_t m = g.minv[j];
-            park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
+            const double invp = g.invp[j], pneg = -(double)p;
+            const double cneg = __builtin_fma(-0x1p52, invp, 0x1p-8);
+            park([&](int x) { return residue_biased_f64((uint32_t)x, invp, cneg, pneg); });
         } else {
             const int bar = g.barrett[j];
             const bool p256 = (p == 256);  // modulus 256: the low byte (conv_32i_2_8u.hpp:7-20)
@@ -573,7 +588,11 @@ template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArg
 // SIMD, item 4); 0 = priority 1 around every MFMA interval (as the one-tile kernel); 2 = no priority
 // changes.  Measured in one process (tools/probes/persist_prio.hip, random bytes): 1 and 2 are
 // 0.3-0.8 % faster than 0 at 8192^3, 4096^3 and 8192^2 x 1024, with identical residues.
-template <bool SUB, int PRIO = 1>
+// EPIM (A/B probes): 0 = the f64 form of the biased residue (default; residue_biased_f64, the low byte
+// for p = 256), 1 = the low byte only (wrong residues: the cost of the reduction), 2 = the integer form
+// (residue_biased).  Measured in one process (tools/probes/persist_epim.hip): the reduction costs 2 % of
+// the cfg2 products and 6-10 % at k = 1024-2048; the f64 form is 0.5-1 % faster than the integer one.
+template <bool SUB, int PRIO = 1, int EPIM = 0>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArgs g) {
     __shared__ __attribute__((aligned(1024))) int8_t smem[LDS_BYTES + PARK_SPARE];
     static_assert(LDS_BYTES + PARK_SPARE <= 160 * 1024, "LDS");
@@ -718,7 +737,13 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
                     }
                 }
         };
-        if (g.biased) {
+        if (EPIM == 1 || (g.biased && p == 256)) {  // (EPIM 1: probe ablation) p = 256: bias is a multiple of 256
+            park([&](int x) { return (uint32_t)x & 0xffu; });
+        } else if (EPIM == 0 && g.biased) {
+            const double invp = g.invp[ct.j], pneg = -(double)p;
+            const double cneg = __builtin_fma(-0x1p52, invp, 0x1p-8);
+            park([&](int x) { return residue_biased_f64((uint32_t)x, invp, cneg, pneg); });
+        } else if (g.biased) {
             const uint32_t m = g.minv[ct.j];
             park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
         } else {
@@ -756,7 +781,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
 __global__ void residue_selftest_kernel(int path, GemmArgs g, unsigned long long *count) {
     unsigned long long bad = 0;
     // path 2: the biased check against a deliberately wrong expectation (negative control: every
-    // pair must be counted)
+    // pair must be counted); path 3: the f64 form of the biased residue (p < 256; 256: the low byte)
     const uint64_t total = path != 1 ? ((uint64_t)1 << 31) + 1 : ((uint64_t)1 << 32);
     const int64_t lo = path != 1 ? -((int64_t)1 << 30) : -((int64_t)1 << 31);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -770,8 +795,15 @@ __global__ void residue_selftest_kernel(int path, GemmArgs g, unsigned long long
             if (r >= p) r -= p;
             if (path == 2) r = (r + 1) % p;
             uint32_t got;
-            if (path != 1) got = residue_biased((uint32_t)((int32_t)x + g.bias[j]), (uint32_t)p, g.minv[j]);
-            else got = residue((int)x, g.p[j], g.barrett[j], p == 256);
+            if (path == 3) {
+                const uint32_t u = (uint32_t)((int32_t)x + g.bias[j]);
+                got = p == 256 ? (u & 0xffu)
+                               : residue_biased_f64(u, g.invp[j], __builtin_fma(-0x1p52, g.invp[j], 0x1p-8), -(double)p);
+            } else if (path != 1) {
+                got = residue_biased((uint32_t)((int32_t)x + g.bias[j]), (uint32_t)p, g.minv[j]);
+            } else {
+                got = residue((int)x, g.p[j], g.barrett[j], p == 256);
+            }
             bad += (got != (uint32_t)r);
         }
     }
@@ -788,6 +820,7 @@ unsigned long long residue_selftest(int path, hipStream_t st) {
         const uint32_t p = MP.p[i] > 0 ? (uint32_t)MP.p[i] : 256u;
         g.minv[i] = (uint32_t)((((uint64_t)1) << 32) / p);
         g.bias[i] = (int)(((((uint64_t)1) << 30) + p - 1) / p * p);
+        g.invp[i] = 1.0 / (double)p;
     }
     unsigned long long *d = nullptr, h = ~0ull;
     if (hipMalloc(&d, sizeof(h)) != hipSuccess) return h;
@@ -819,6 +852,7 @@ static unsigned device_cu_count() {
 // persistent when the launch has at least four tiles per CU.  g_persistent_override (probes) wins when >= 0.
 int g_persistent_override = -1;
 int g_prio_override = 1;  // probes: the persistent kernel's priority variant (PRIO; 1 = the default)
+int g_epim_override = 0;  // probes: the persistent kernel's residue arithmetic (EPIM; 0 = the default)
 static int persistent_mode() {
     if (g_persistent_override >= 0) return g_persistent_override;
     static const int env = [] {
@@ -857,6 +891,7 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         const uint32_t p = MP.p[i] > 0 ? (uint32_t)MP.p[i] : 256u;
         g.minv[i] = (uint32_t)((((uint64_t)1) << 32) / p);
         g.bias[i] = (int)(((((uint64_t)1) << 30) + p - 1) / p * p);
+        g.invp[i] = 1.0 / (double)p;
     }
     g.kstride = g.ksteps;
     g.k0 = 0;
@@ -907,6 +942,8 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
         if (g.nsub == 3) gemm_i8_persistent_kernel<true, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        else if (g_epim_override == 1) gemm_i8_persistent_kernel<false, 1, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        else if (g_epim_override == 2) gemm_i8_persistent_kernel<false, 1, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else if (g_prio_override == 0) gemm_i8_persistent_kernel<false, 0><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else if (g_prio_override == 2) gemm_i8_persistent_kernel<false, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else gemm_i8_persistent_kernel<false, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);

@@ -434,11 +434,12 @@ def test_padded_leading_dimensions(fast):
     assert np.all(Cg[m:] == 7.0)
 
 
-@pytest.mark.parametrize("path", [0, 1])
+@pytest.mark.parametrize("path", [0, 1, 3])
 def test_residue_epilogue_exhaustive(path):
-    """every input of both residue reductions of the product epilogue, all 20 moduli, against exact
-    arithmetic: the biased form over x in [-2^30, 2^30] (k_pad <= 2^16) and the reference's signed
-    Barrett step (conv_32i_2_8u.hpp:7-56) over every int32 -- 8.6e10 and 1.7e11 checks"""
+    """every input of the residue reductions of the product epilogue, all 20 moduli, against exact
+    arithmetic: the biased form over x in [-2^30, 2^30] (k_pad <= 2^16) as integer Barrett (path 0) and
+    as the f64 form the kernels use (path 3), and the reference's signed Barrett step
+    (conv_32i_2_8u.hpp:7-56) over every int32 (path 1) -- 4.3e10, 4.3e10 and 8.6e10 checks"""
     import ctypes
     import gemmul8 as G
     G.lib.gemmul8_residue_selftest.restype = ctypes.c_ulonglong
