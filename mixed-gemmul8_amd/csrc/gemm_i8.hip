@@ -77,10 +77,8 @@ struct GemmArgs {
     // these strides in the A, B and output planes
     unsigned nsub;
     size_t subA, subB, subOut;
-    // persistent kernel: planes of the launch (sub-products counted) and the bytes of the A and B
-    // regions its buffer descriptors cover (< 4 GiB)
+    // persistent kernel: planes of the launch (sub-products counted)
     unsigned nplanes;
-    uint32_t regionA, regionB;
     uint32_t *queue;  // 8 per-XCD tile-queue heads, zeroed before the launch
 };
 
@@ -556,7 +554,7 @@ constexpr unsigned NO_TILE = 0xffffffffu;
 
 struct TileRef {
     unsigned j, sb, tm, tn;
-    uint32_t offA, offB;  // byte offsets of the tile's k-step 0 panel in the A and B regions
+    uint32_t offA, offB;  // byte offsets of the tile's k-step 0 panel in its modulus's A and B planes
 };
 
 template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArgs &g, unsigned u) {
@@ -571,8 +569,8 @@ template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArg
     const unsigned idx = v - grp * GM * g.ntiles;
     t.tm = grp * GM + idx % gm;
     t.tn = idx / gm;
-    t.offA = (uint32_t)(t.j * g.planeA + t.sb * g.subA + (size_t)t.tm * g.kstride * PANEL);
-    t.offB = (uint32_t)(t.j * g.planeB + t.sb * g.subB + (size_t)t.tn * g.kstride * PANEL);
+    t.offA = (uint32_t)(t.sb * g.subA + (size_t)t.tm * g.kstride * PANEL);
+    t.offB = (uint32_t)(t.sb * g.subB + (size_t)t.tn * g.kstride * PANEL);
     // block-uniform: keep them in SGPRs (the compiler's divergence analysis does not see it)
     t.j = __builtin_amdgcn_readfirstlane(t.j);
     t.sb = __builtin_amdgcn_readfirstlane(t.sb);
@@ -628,13 +626,16 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
     const unsigned K = g.ksteps;
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
     const uint32_t lds_wave = lds_base + wave * 1024;
-    const v4si rA = make_rsrc(g.A, g.regionA);
-    const v4si rB = make_rsrc(g.B, g.regionB);
     const uint32_t lane_off = wave * 1024 + lane * 16;
+    // buffer descriptors of one modulus's A and B planes (each < 4 GiB; the launch's planes together
+    // may exceed it): the DMA switches to the successor tile's descriptors with its cursor
+    auto rsrcA = [&](const TileRef &t) { return make_rsrc(g.A + (size_t)t.j * g.planeA, (uint32_t)g.planeA); };
+    auto rsrcB = [&](const TileRef &t) { return make_rsrc(g.B + (size_t)t.j * g.planeB, (uint32_t)g.planeB); };
     auto lo_of = [&](unsigned step) { return lds_wave + (step & (STAGES - 1)) * SLOT; };
     auto rd_of = [&](unsigned step) { return smem + (step & (STAGES - 1)) * SLOT; };
 
     TileRef ct = decode_tile<SUB>(g, tile_u(ccur));
+    v4si rA = rsrcA(ct), rB = rsrcB(ct);  // descriptors of the DMA cursor
     constexpr unsigned D = STAGES - 1;
     for (unsigned s0 = 0; s0 < D; ++s0) {  // steps 0..2 of the first tile
         const uint32_t lo = lo_of(s0);
@@ -660,6 +661,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
         if (wr == 1) barrier();  // group 1 falls one barrier behind (ping-pong, as in the one-tile kernel)
         unsigned k = 0;
         uint32_t na = 0, nb = 0;  // the next tile's step-0 panels
+        v4si nrA = rA, nrB = rB;  // and its descriptors
         // one k-step: reads of slot s, DMA of step s+3 (this tile's step k+3, or the next tile's step
         // k+3-K once k+3 >= K: the cursor jumps there after staging this tile's last step), wait, MFMAs
         auto step = [&](auto wait) {
@@ -673,6 +675,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             const bool jump = k + D + 1 == K;
             da = jump ? na : da + PANEL;
             db = jump ? nb : db + PANEL;
+            if (jump) {  // block-uniform
+                rA = nrA;
+                rB = nrB;
+            }
             wait();
             barrier();
             mfma_step<PRIO>(acc, f);
@@ -688,6 +694,8 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             nt = decode_tile<SUB>(g, tile_u(cnext));
             na = nt.offA;
             nb = nt.offB;
+            nrA = rsrcA(nt);
+            nrB = rsrcB(nt);
         }
         // steady steps; the block's last tile stops staging three steps before its end
         const unsigned kend = cnext != NO_TILE ? K : K - D;
@@ -919,19 +927,15 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         }
         return;
     }
-    // persistent residue kernel: a tile-queue area, whole-region buffer descriptors (< 4 GiB),
+    // persistent residue kernel: a tile-queue area, buffer descriptors (planes < 4 GiB),
     // >= 6 k-steps per tile (the kernel's cursor jump at k = K - 4 after its first two steps) and, by default, >= 4 tiles per CU (measured, same process: cfg2 products 5.16 -> 5.04 ms,
     // 8192^2 x 1024 1.14 -> 1.01 ms, 4096^3 0.857 -> 0.842 ms; at 2048^3, 3.5 tiles per CU, the
     // queue-zeroing launch costs more than the persistent kernel saves: 0.115 -> 0.118 ms)
     const unsigned ntiles_all = (unsigned)(L.mtiles * L.ntiles) * nplanes * g.nsub;
-    const size_t regA = (size_t)nplanes * L.planeA, regB = (size_t)nplanes * L.planeB;
     const unsigned ncu = device_cu_count();
     const int pmode = persistent_mode();
-    if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && regA < ((size_t)1 << 32) &&
-        regB < ((size_t)1 << 32) && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 4 * ncu)) {
+    if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 4 * ncu)) {
         g.nplanes = nplanes * g.nsub;
-        g.regionA = (uint32_t)regA;
-        g.regionB = (uint32_t)regB;
         g.queue = queue;
         zero_i32(reinterpret_cast<int32_t *>(queue), 8, st);
         // GEMMUL8_PERSISTENT_GRID caps the grid (tests: many tiles per block at small shapes), at no fewer

@@ -640,3 +640,35 @@ def test_persistent_default_matches_one_tile():
             outs.append(np.load(out))
         for k in outs[0].files:
             assert np.array_equal(outs[0][k].view(np.uint64), outs[1][k].view(np.uint64)), k
+
+
+def test_persistent_planes_beyond_4gib():
+    """A launch whose 14 A slice planes span more than 4 GiB (m = 20480, k = 15360: 315 MB per plane):
+    the persistent kernel addresses each modulus's plane with its own buffer descriptor and switches
+    descriptors with its DMA cursor; C bit-identical to the one-tile kernel (GEMMUL8_PERSISTENT=0)."""
+    import subprocess
+    import tempfile
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    code = ("import sys, numpy as np, torch; sys.path[:0] = sys.argv[1:3]\n"
+            "import gemmul8 as G\n"
+            "m, n, k, N = 20480, 256, 15360, 14\n"
+            "assert N * G.layout(m, n, k, N)['planeA'] > (1 << 32)\n"
+            "g = torch.Generator(device='cuda'); g.manual_seed(5)\n"
+            "A = torch.randn((k, m), dtype=torch.float64, device='cuda', generator=g)\n"
+            "B = torch.randn((n, k), dtype=torch.float64, device='cuda', generator=g)\n"
+            "C = torch.empty((n, m), dtype=torch.float64, device='cuda')\n"
+            "W = G.alloc_work(m, n, k, N)\n"
+            "G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, True, W)\n"
+            "np.save(sys.argv[3], C.cpu().numpy())\n")
+    with tempfile.TemporaryDirectory() as d:
+        outs = []
+        for mode in ("0", ""):
+            out = os.path.join(d, f"c{mode or 'default'}.npy")
+            env = dict(os.environ, GEMMUL8_PERSISTENT=mode) if mode else {
+                kk: v for kk, v in os.environ.items() if kk != "GEMMUL8_PERSISTENT"}
+            r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "mixed-gemmul8_amd"), tdir, out],
+                               env=env, capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0, r.stderr[-3000:]
+            outs.append(np.load(out))
+        assert np.array_equal(outs[0].view(np.uint64), outs[1].view(np.uint64))
