@@ -594,7 +594,7 @@ template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArg
 #ifndef OZ2_STAMPS
 #define OZ2_STAMPS 0  // probe builds only (tools/probes/persist_stamps.hip): s_memtime phase sums per wave
 #endif
-template <bool SUB, int PRIO = 1, int EPIM = 0, int EPIL = 0>
+template <bool SUB, int PRIO = 1, int EPIM = 0>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArgs g) {
 #if OZ2_STAMPS
     // [0] realign, [1] residues -> LDS, [2] park barrier, [3] stores + barrier, [4] accumulator reset +
@@ -678,16 +678,16 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
         for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
             for (int jj = 0; jj < ACC_J; ++jj) acc[i][jj] = AccTile{} + acc0;
-        // group 1 falls one barrier behind (ping-pong, as in the one-tile kernel); with the barrier-free
-        // epilogue (EPIL 1) it stays behind across tiles
-        if (wr == 1 && (EPIL == 0 || r == 0)) barrier();
+        if (wr == 1) barrier();  // group 1 falls one barrier behind (ping-pong, as in the one-tile kernel)
         OZ2_STAMP(4);
         unsigned k = 0;
         uint32_t na = 0, nb = 0;  // the next tile's step-0 panels
         v4si nrA = rA, nrB = rB;  // and its descriptors
         // one k-step: reads of slot s, DMA of step s+3 (this tile's step k+3, or the next tile's step
         // k+3-K once k+3 >= K: the cursor jumps there after staging this tile's last step), wait, MFMAs
-        auto stage_ahead = [&]() {  // the DMA of step s + D, then the cursor moves on
+        auto step = [&](auto wait) {
+            read_frags(f, rd_of(s), wr, wc, lane);
+            __builtin_amdgcn_sched_barrier(0);
             const uint32_t lo = lo_of(s + D);
             bglds16(rA, da + lane_off, lo);
             bglds16(rA, da + lane_off + 8192, lo + 8192);
@@ -700,11 +700,6 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
                 rA = nrA;
                 rB = nrB;
             }
-        };
-        auto step = [&](auto wait, auto dma) {
-            read_frags(f, rd_of(s), wr, wc, lane);
-            __builtin_amdgcn_sched_barrier(0);
-            if constexpr (decltype(dma)::value) stage_ahead();
             wait();
             barrier();
             mfma_step<PRIO>(acc, f);
@@ -712,12 +707,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
         };
         if (r > 0) {
             // steps 0 and 1: the previous tile's 8 residue stores are younger than the awaited DMA
-            // (the barrier-free epilogue staged step 0's DMA before it)
-            step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1) + (EPIL == 2 ? 0 : PARK_STORES)>(); },
-                 std::integral_constant<bool, EPIL == 0>{});
+            step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1) + PARK_STORES>(); });
             ++k, ++s;
             OZ2_STAMP(5);
-            step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1) + (EPIL == 2 ? 0 : PARK_STORES)>(); }, std::true_type{});
+            step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1) + PARK_STORES>(); });
             ++k, ++s;
             OZ2_STAMP(6);
             cnext = __builtin_amdgcn_readfirstlane(spare[0]);  // written by wave 0 two barriers ago
@@ -732,7 +725,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
         }
         // steady steps; the block's last tile stops staging three steps before its end
         const unsigned kend = cnext != NO_TILE ? K : K - D;
-        for (; k < kend; ++k, ++s) step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>(); }, std::true_type{});
+        for (; k < kend; ++k, ++s) step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>(); });
         for (; k < K; ++k, ++s) {  // drain of the block's last tile
             read_frags(f, rd_of(s), wr, wc, lane);
             __builtin_amdgcn_sched_barrier(0);
@@ -742,79 +735,6 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             barrier();
         }
         OZ2_STAMP(7);
-        if constexpr (EPIL >= 1) {
-            // Barrier-free epilogue: the residues go from the accumulators straight to 16-byte stores.
-            // A 16x16 accumulator tile gives lane (g, c) = (lane >> 4, lane & 15) rows 4g..4g+3 of column
-            // c; for four row tiles i0..i0+3 of one column block, two v_permlane32_swap and two
-            // v_permlane16_swap transpose the four packed dwords across the lane groups so that lane
-            // (g, c) holds rows 16 (i0 + g) .. +15 of column c: one 16-byte store, no LDS, no barrier.
-            // Group 0 runs it while group 1 finishes its last MFMA interval, group 1 while group 0
-            // starts the next tile: the ping-pong carries on across the tile boundary.
-            // the next tile's step-3 DMA first (step 0 of the next tile skips it): the slot is free (both
-            // groups read it before their last MFMA interval), and a group's epilogue must not hold back
-            // its share of the prefetch (issued after it, the pieces of one group trailed the other's
-            // by the whole epilogue and the next tile's first k-steps waited for them)
-            if (cnext != NO_TILE) stage_ahead();
-            unsigned pos = 0;
-            const bool claiming = tid == 0 && cnext != NO_TILE;
-            if (claiming) pos = claim();
-            if (PRIO == 1 && wr == 1) __builtin_amdgcn_s_setprio(0);  // the partner's MFMAs issue first
-            int etid = tid;
-            asm volatile("" : "+v"(etid));
-            const int elane = etid & 63;
-            const int p = g.p[ct.j];
-            uint8_t *const out = static_cast<uint8_t *>(g.out) + ct.j * g.planeOut + ct.sb * g.subOut +
-                                 ((size_t)ct.tn * 256 + wc * 64 + (elane & 15)) * g.ldo + (size_t)ct.tm * 256 +
-                                 wr * 128 + (elane >> 4) * 16;
-            auto emit = [&](auto &&res) {
-#pragma unroll
-                for (int jj = 0; jj < ACC_J; ++jj)
-#pragma unroll
-                    for (int h = 0; h < 2; ++h) {
-                        uint32_t x[4];
-#pragma unroll
-                        for (int t = 0; t < 4; ++t) {
-                            const AccTile &a = acc[4 * h + t][jj];
-                            x[t] = res(a[0]) | (res(a[1]) << 8) | (res(a[2]) << 16) | (res(a[3]) << 24);
-                        }
-                        auto s02 = __builtin_amdgcn_permlane32_swap(x[0], x[2], false, false);
-                        auto s13 = __builtin_amdgcn_permlane32_swap(x[1], x[3], false, false);
-                        auto s01 = __builtin_amdgcn_permlane16_swap(s02[0], s13[0], false, false);
-                        auto s23 = __builtin_amdgcn_permlane16_swap(s02[1], s13[1], false, false);
-                        if (EPIL == 2)  // probe ablation: no residue stores
-                            asm volatile("" ::"v"(s01[0]), "v"(s01[1]), "v"(s23[0]), "v"(s23[1]));
-                        else
-                            *reinterpret_cast<uint4 *>(out + (size_t)(jj * 16) * g.ldo + h * 64) =
-                                make_uint4(s01[0], s01[1], s23[0], s23[1]);
-                    }
-            };
-            if (EPIM == 1 || (g.biased && p == 256)) {
-                emit([&](int x) { return (uint32_t)x & 0xffu; });
-            } else if (EPIM == 0 && g.biased) {
-                const double invp = g.invp[ct.j], pneg = -(double)p;
-                const double cneg = __builtin_fma(-0x1p52, invp, 0x1p-8);
-                emit([&](int x) { return residue_biased_f64((uint32_t)x, invp, cneg, pneg); });
-            } else if (g.biased) {
-                const uint32_t m = g.minv[ct.j];
-                emit([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
-            } else {
-                const int bar = g.barrett[ct.j];
-                const bool p256 = (p == 256);
-                emit([&](int x) { return residue(x, p, bar, p256); });
-            }
-            if (PRIO == 1 && wr == 1) __builtin_amdgcn_s_setprio(1);
-            OZ2_STAMP(1);
-#if OZ2_STAMPS
-            st_acc[8] += 1;
-#endif
-            if (tid == 0) spare[0] = claiming ? to_tile(pos) : NO_TILE;  // read at the next tile's k = 1
-            if (cnext == NO_TILE) {
-                if (wr == 0) barrier();  // group 1's last MFMA interval ends at this barrier
-                break;
-            }
-            ct = nt;
-            continue;
-        }
         if (wr == 0) barrier();  // realign the groups
         barrier();
         OZ2_STAMP(0);
@@ -981,7 +901,6 @@ int g_persistent_override = -1;
 int g_prio_override = 1;  // probes: the persistent kernel's priority variant (PRIO; 1 = the default)
 int g_epim_override = 0;  // probes: the persistent kernel's residue arithmetic (EPIM; 0 = the default)
 unsigned long long *g_stamps = nullptr;  // probes: OZ2_STAMPS builds' per-wave phase sums
-int g_epil_override = 0;  // probes: the persistent kernel's epilogue (EPIL; 0 = LDS park, 1 = barrier-free)
 static int persistent_mode() {
     if (g_persistent_override >= 0) return g_persistent_override;
     static const int env = [] {
@@ -1068,8 +987,6 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
         if (g.nsub == 3) gemm_i8_persistent_kernel<true, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else if (g_epil_override == 1) gemm_i8_persistent_kernel<false, 1, 0, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else if (g_epil_override == 2) gemm_i8_persistent_kernel<false, 1, 0, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else if (g_epim_override == 1) gemm_i8_persistent_kernel<false, 1, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else if (g_epim_override == 2) gemm_i8_persistent_kernel<false, 1, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
         else if (g_prio_override == 0) gemm_i8_persistent_kernel<false, 0><<<pgrid, dim3(NTHREADS), 0, st>>>(g);

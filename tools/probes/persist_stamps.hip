@@ -2,8 +2,8 @@
 // s_memtime deltas per wave over [0] realign barriers, [1] residues -> LDS, [2] park barrier,
 // [3] residue stores + barrier, [4] accumulator reset + stagger barrier, [5] k-step 0, [6] k-step 1,
 // [7] the other k-steps; printed per tile, averaged over blocks, for wave 0 (group 0) and wave 4
-// (group 1).  Random operand bytes, cfg2-shaped launch (m = n from argv[3], N, k from argv);
-// argv[4] = 1: the barrier-free epilogue (EPIL 1), whose whole epilogue lands in slot [1].
+// (group 1).  Random operand bytes, cfg2-shaped launch (m = n from argv[3], N, k from argv).
+// (The barrier-free epilogue variant it was also run on lives in git history, commit 39a29fd.)
 #define OZ2_STAMPS 1
 #include "../../mixed-gemmul8_amd/csrc/gemm_i8.hip"
 #include <cstdio>
@@ -28,7 +28,6 @@ int main(int argc, char **argv) {
     const unsigned N = argc > 1 ? atoi(argv[1]) : 14;
     const size_t k = argc > 2 ? atoll(argv[2]) : 8192;
     const size_t m = argc > 3 ? atoll(argv[3]) : 8192, n = m;
-    oz2::g_epil_override = argc > 4 ? atoi(argv[4]) : 0;  // 1: the barrier-free epilogue (its E in slot [1])
     oz2::Layout L = oz2::make_layout(m, n, k, N, false);
     void *w;
     if (hipMalloc(&w, L.total) != hipSuccess) return 1;
