@@ -97,7 +97,7 @@ def cpu_baseline(size_hint):
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     threads = O.num_threads()
-    n = size_hint or 4096
+    n = size_hint or 5120  # about 14 s of the oracle on 16 host threads (6.9 s at 4096)
     rng = np.random.default_rng(123456)
     A = np.asfortranarray((1.0 - rng.random((n, n)) - 0.5) * np.exp(0.5 * rng.standard_normal((n, n))))
     t0 = time.perf_counter()
