@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
 
 template <int OT, bool NUMM1, unsigned N, bool KARA>
 static void launch_crt_n(const CrtArgs &a, dim3 grid, hipStream_t st) {
-    crt_kernel<OT, NUMM1, N, KARA><<<grid, dim3(256), 0, st>>>(a);
+    launch(crt_kernel<OT, NUMM1, N, KARA>, grid, dim3(256), st, a);
 }
 
 template <int OT, bool NUMM1, bool KARA = false>

@@ -947,8 +947,8 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     // GEMMUL8_FORCE_FLAT_DMA=1 takes the 64-bit path at any size (tests cover it with small shapes)
     const char *ff = getenv("GEMMUL8_FORCE_FLAT_DMA");
     const bool buf = L.planeA < ((size_t)1 << 32) && L.planeB < ((size_t)1 << 32) && !(ff && atoi(ff));
-#define OZ2_GEMM1(E, B) gemm_i8_kernel<E, B><<<grid, dim3(NTHREADS), 0, st>>>(g)
-#define OZ2_GEMM(E, B) (g.nsub == 3 ? (void)(gemm_i8_kernel<E, B, true><<<grid, dim3(NTHREADS), 0, st>>>(g)) : (void)OZ2_GEMM1(E, B))
+#define OZ2_GEMM1(E, B) launch(gemm_i8_kernel<E, B>, grid, dim3(NTHREADS), st, g)
+#define OZ2_GEMM(E, B) (g.nsub == 3 ? launch(gemm_i8_kernel<E, B, true>, grid, dim3(NTHREADS), st, g) : OZ2_GEMM1(E, B))
     // beyond k_pad = 2^17 an int32 product can wrap (the reference's int32 C32i does): the residue
     // product then runs in k-chunks of 2^16 (biased path), each adding its residues into the planes
     // mod p.  GEMMUL8_KCHUNK (k-steps, multiple of 1) forces chunking at small k for the tests.
@@ -986,12 +986,12 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
             return e ? (unsigned)atoi(e) : 0u;
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
-        if (g.nsub == 3) gemm_i8_persistent_kernel<true, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else if (g_epim_override == 1) gemm_i8_persistent_kernel<false, 1, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else if (g_epim_override == 2) gemm_i8_persistent_kernel<false, 1, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else if (g_prio_override == 0) gemm_i8_persistent_kernel<false, 0><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else if (g_prio_override == 2) gemm_i8_persistent_kernel<false, 2><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
-        else gemm_i8_persistent_kernel<false, 1><<<pgrid, dim3(NTHREADS), 0, st>>>(g);
+        if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
+        else if (g_epim_override == 1) launch(gemm_i8_persistent_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
+        else if (g_epim_override == 2) launch(gemm_i8_persistent_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
+        else if (g_prio_override == 0) launch(gemm_i8_persistent_kernel<false, 0>, pgrid, dim3(NTHREADS), st, g);
+        else if (g_prio_override == 2) launch(gemm_i8_persistent_kernel<false, 2>, pgrid, dim3(NTHREADS), st, g);
+        else launch(gemm_i8_persistent_kernel<false, 1>, pgrid, dim3(NTHREADS), st, g);
         return;
     }
     switch (epi) {

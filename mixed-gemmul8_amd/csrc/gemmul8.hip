@@ -138,12 +138,14 @@ static void join(const Call &c) {
 }
 
 // ---------------- phase timing (HIP events on the call's stream) ----------------
+
 namespace timing {
 static std::mutex mu;
 static bool enabled = false;
 struct Rec {
-    hipEvent_t ev[4];  // after split, after products, (conversion = products), after crt
-    hipEvent_t start;
+    // split start (its first launch), products start / end, CRT end; prod_only: gemmul8_products
+    hipEvent_t start, prod0, prod1, crt1;
+    bool prod_only;
 };
 static std::vector<Rec> pending;
 static std::vector<Rec> pool;
@@ -151,31 +153,59 @@ static double acc_ms[4] = {0, 0, 0, 0};
 static int calls = 0;
 
 static Rec acquire() {
-    Rec r;
+    Rec r{};
     if (!pool.empty()) {
         r = pool.back();
         pool.pop_back();
+        r.prod_only = false;
         return r;
     }
     (void)hipEventCreate(&r.start);
-    for (auto &e : r.ev) (void)hipEventCreate(&e);
+    (void)hipEventCreate(&r.prod0);
+    (void)hipEventCreate(&r.prod1);
+    (void)hipEventCreate(&r.crt1);
     return r;
+}
+static float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0;
+    return hipEventElapsedTime(&ms, a, b) == hipSuccess ? ms : 0.f;
+}
+// phase times of one call in ms: split, products, (conversion: fused), CRT
+static void read(const Rec &r, float out[4]) {
+    (void)hipEventSynchronize(r.prod_only ? r.prod1 : r.crt1);
+    out[0] = r.prod_only ? 0.f : elapsed(r.start, r.prod0);
+    out[1] = elapsed(r.prod0, r.prod1);
+    out[2] = 0.f;
+    out[3] = r.prod_only ? 0.f : elapsed(r.prod1, r.crt1);
 }
 static void resolve_all() {
     for (auto &r : pending) {
-        (void)hipEventSynchronize(r.ev[3]);
-        float a = 0, b = 0, c = 0;
-        (void)hipEventElapsedTime(&a, r.start, r.ev[0]);
-        (void)hipEventElapsedTime(&b, r.ev[0], r.ev[1]);
-        (void)hipEventElapsedTime(&c, r.ev[2], r.ev[3]);
-        acc_ms[0] += a;
-        acc_ms[1] += b;
-        acc_ms[3] += c;
+        float t[4];
+        read(r, t);
+        for (int i = 0; i < 4; ++i) acc_ms[i] += t[i];
         ++calls;
         pool.push_back(r);
     }
     pending.clear();
 }
+
+// arms the events of one phase for launch() on stream st; end() records, as markers, whichever of
+// them no launch took (a phase with no kernel on that stream), so every event of a call is recorded
+struct Phase {
+    bool on;
+    Phase(bool record, hipStream_t st, hipEvent_t start, hipEvent_t stop) : on(record) {
+        if (on) g_phase_ev = PhaseEvents{st, start, stop, false};
+    }
+    void end() {
+        if (!on) return;
+        PhaseEvents &e = g_phase_ev;
+        if (e.start) (void)hipEventRecord(e.start, e.st);
+        if (e.stop && !e.stop_taken) (void)hipEventRecord(e.stop, e.st);
+        g_phase_ev = PhaseEvents{};
+        on = false;
+    }
+    ~Phase() { g_phase_ev = PhaseEvents{}; }  // failure paths: nothing left armed
+};
 }  // namespace timing
 
 // Launch errors: every entry point that enqueues work first clears an error left pending on the
@@ -331,7 +361,6 @@ static int run(Call &c, double *phase_ns) {
         record = want_events || (timing::enabled && !capturing);
         if (record) rec = timing::acquire();
     }
-    if (record) (void)hipEventRecord(rec.start, c.st);
 
     // a failed launch ends the call before the next phase is enqueued (the events recorded so far
     // go back to the pool unread)
@@ -344,21 +373,26 @@ static int run(Call &c, double *phase_ns) {
     };
     const unsigned S = v.L.S;
     if (S >= c.N) {
+        timing::Phase split(record, c.st, rec.start, nullptr);
         phase_split(c, v, 0, c.N, false);
+        split.end();
         if (!launch_ok()) return fail();
-        if (record) (void)hipEventRecord(rec.ev[0], c.st);
+        timing::Phase prod(record, c.st, rec.prod0, rec.prod1);
         phase_products(v, c.N, 0, c.N, 0, c.st);
+        prod.end();
         if (!launch_ok()) return fail();
     } else {
         // low-memory mode: the moduli in groups of S through the same S slice planes (each group
         // re-reads A and B); the product phase timer then includes the re-encoding
+        timing::Phase split(record, c.st, rec.start, nullptr);
         if (!c.fast) phase_bound(c, v);
         fork(c);
         operand_shifts(c, v, true, c.st);
         operand_shifts(c, v, false, c.stB);
         join(c);
+        split.end();
         if (!launch_ok()) return fail();
-        if (record) (void)hipEventRecord(rec.ev[0], c.st);
+        timing::Phase prod(record, c.st, rec.prod0, rec.prod1);
         for (unsigned j0 = 0; j0 < c.N; j0 += S) {
             const unsigned j1 = j0 + S < c.N ? j0 + S : c.N;
             fork(c);
@@ -369,26 +403,20 @@ static int run(Call &c, double *phase_ns) {
             phase_products(v, c.N, j0, j1, 0, c.st);
             if (!launch_ok()) return fail();
         }
-    }
-    if (record) {
-        (void)hipEventRecord(rec.ev[1], c.st);
-        (void)hipEventRecord(rec.ev[2], c.st);
+        prod.end();
     }
 
-    phase_crt(v, c.N, c.ot, c.alpha, c.beta, c.C, c.ldc, c.st);
+    {
+        timing::Phase crt(record, c.st, nullptr, rec.crt1);
+        phase_crt(v, c.N, c.ot, c.alpha, c.beta, c.C, c.ldc, c.st);
+        crt.end();
+    }
     if (!launch_ok()) return fail();
-    if (record) (void)hipEventRecord(rec.ev[3], c.st);
 
     if (want_events) {
-        (void)hipEventSynchronize(rec.ev[3]);
-        float a = 0, b = 0, d = 0;
-        (void)hipEventElapsedTime(&a, rec.start, rec.ev[0]);
-        (void)hipEventElapsedTime(&b, rec.ev[0], rec.ev[1]);
-        (void)hipEventElapsedTime(&d, rec.ev[2], rec.ev[3]);
-        phase_ns[0] = a * 1e6;
-        phase_ns[1] = b * 1e6;
-        phase_ns[2] = 0.0;
-        phase_ns[3] = d * 1e6;
+        float t[4];
+        timing::read(rec, t);
+        for (int i = 0; i < 4; ++i) phase_ns[i] = t[i] * 1e6;
     }
     if (record) {
         std::lock_guard<std::mutex> g(timing::mu);
@@ -527,23 +555,21 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
     oz2::clear_stale_error();
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // with timing enabled the launch is bracketed like gemmul8_gemm's product phase (phases 0/3 read 0)
+    // with timing enabled the launch is timed like gemmul8_gemm's product phase (phases 0/3 read 0)
     bool record;
     oz2::timing::Rec rec{};
     {
         std::lock_guard<std::mutex> g(oz2::timing::mu);
         record = oz2::timing::enabled && !oz2::is_capturing(st);
-        if (record) rec = oz2::timing::acquire();
+        if (record) {
+            rec = oz2::timing::acquire();
+            rec.prod_only = true;
+        }
     }
-    if (record) {
-        (void)hipEventRecord(rec.start, st);
-        (void)hipEventRecord(rec.ev[0], st);
-    }
+    oz2::timing::Phase prod(record, st, rec.prod0, rec.prod1);
     oz2::phase_products(v, num_moduli, mod_begin, mod_end, mod_begin, st);
+    prod.end();
     if (record) {
-        (void)hipEventRecord(rec.ev[1], st);
-        (void)hipEventRecord(rec.ev[2], st);
-        (void)hipEventRecord(rec.ev[3], st);
         std::lock_guard<std::mutex> g(oz2::timing::mu);
         oz2::timing::pending.push_back(rec);
     }

@@ -1,8 +1,38 @@
 // oz2_split.hpp -- internal launcher interface of the gfx950 kernels.
 #pragma once
+#include <hip/hip_ext.h>
+
 #include "oz2_common.hpp"
 
 namespace oz2 {
+
+// ---- kernel launches and the phase timers ----
+// The phase times (gemm()'s returned ns, bench.py's product-kernel duration) need timestamps at the
+// phase boundaries.  A hipEventRecord between dependent kernels enqueues a marker packet that costs
+// ~3.5 us of stream time on MI355X (tools/probes/event_cost.hip: four kernels with five markers
+// +17.5 us per iteration, the same events attached to the dispatches +4.7 us; a 1024^3 call
+// 60.5 -> 80.4 us with the markers).  So run() arms the events of one phase for the call's stream
+// and every library launch goes through launch(), which attaches them to the dispatches themselves
+// (hipExtLaunchKernel): `start` to the phase's first launch on that stream, `stop` to each of its
+// launches there (the last one's completion stands).
+struct PhaseEvents {
+    hipStream_t st;
+    hipEvent_t start, stop;
+    bool stop_taken;
+};
+inline thread_local PhaseEvents g_phase_ev{};
+
+template <typename... KArgs, typename... Args>
+inline void launch(void (*kernel)(KArgs...), dim3 grid, dim3 block, hipStream_t st, Args... args) {
+    PhaseEvents &e = g_phase_ev;
+    if (e.st == st && (e.start || e.stop)) {
+        hipExtLaunchKernelGGL(kernel, grid, block, 0, st, e.start, e.stop, 0, args...);
+        e.start = nullptr;
+        e.stop_taken = e.stop != nullptr;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+    }
+}
 
 // One operand as the kernels see it: vector v = row of op(A) or column of op(B),
 // element e runs along k.  contig: element e of vector v is at ptr[v*ld + e]

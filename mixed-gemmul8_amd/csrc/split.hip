@@ -740,7 +740,7 @@ __global__ void zero_i32_kernel(int32_t *__restrict__ p, size_t n) {
 void zero_i32(int32_t *p, size_t n, hipStream_t st) {
     if (n == 0) return;
     const size_t blocks = (n + 255) / 256;
-    zero_i32_kernel<<<dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st>>>(p, n);
+    launch(zero_i32_kernel, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), st, p, n);
 }
 
 // ------------------------------------------------------------------
@@ -762,14 +762,14 @@ static void launch_stats(const void *X, size_t ld, bool contig, size_t len, size
                          float log2M, int16_t *out, hipStream_t st) {
     const R *x = static_cast<const R *>(X);
     if (contig) {
-#define OZ2_SC(vt, ac) stats_contig_kernel<R, CPLX, vt, ac><<<dim3((unsigned)nvec), dim3(vt), 0, st>>>(x, ld, len, nvec, log2M, out)
+#define OZ2_SC(vt, ac) launch(stats_contig_kernel<R, CPLX, vt, ac>, dim3((unsigned)nvec), dim3(vt), st, x, ld, len, nvec, log2M, out)
         if (VT == 512) { if (accurate) OZ2_SC(512, true); else OZ2_SC(512, false); }
         else { if (accurate) OZ2_SC(128, true); else OZ2_SC(128, false); }
 #undef OZ2_SC
     } else {
         const int rows = stats_rows(nvec);
         const unsigned g = (unsigned)((nvec + rows - 1) / rows);
-#define OZ2_SS(vt, ac, rw) stats_strided_kernel<R, CPLX, vt, ac, rw><<<dim3(g), dim3(256), 0, st>>>(x, ld, len, nvec, log2M, out)
+#define OZ2_SS(vt, ac, rw) launch(stats_strided_kernel<R, CPLX, vt, ac, rw>, dim3(g), dim3(256), st, x, ld, len, nvec, log2M, out)
 #define OZ2_SSR(vt, ac) do { if (rows == 16) OZ2_SS(vt, ac, 16); else if (rows == 8) OZ2_SS(vt, ac, 8); else OZ2_SS(vt, ac, 4); } while (0)
         if (VT == 512) { if (accurate) OZ2_SSR(512, true); else OZ2_SSR(512, false); }
         else { if (accurate) OZ2_SSR(128, true); else OZ2_SSR(128, false); }
@@ -791,7 +791,7 @@ static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, si
     const dim3 grid = kf ? dim3((unsigned)(L.kblk / KT), (unsigned)(vpad_grid / 64))
                          : dim3((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
     const ModGroups G = make_groups(MP, L.N);  // grouping by the call's N (magnitude bound), not the sub-range
-#define OZ2_EN(cg, md) encode_kernel<R, CPLX, cg, IS_A, md><<<grid, dim3(NT), 0, st>>>(x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G)
+#define OZ2_EN(cg, md) launch(encode_kernel<R, CPLX, cg, IS_A, md>, grid, dim3(NT), st, x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G)
     if (contig) { if (mode == 0) OZ2_EN(true, 0); else OZ2_EN(true, 1); }
     else { if (mode == 0) OZ2_EN(false, 0); else OZ2_EN(false, 1); }
 #undef OZ2_EN
@@ -836,7 +836,7 @@ bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, si
     const int rows = stats_rows(m);
     const unsigned ga = (unsigned)((m + rows - 1) / rows), gb = (unsigned)((n + 1) / 2);
     const double *a = static_cast<const double *>(dA.ptr), *b = static_cast<const double *>(dB.ptr);
-#define OZ2_SP(r) stats_pair_kernel<r><<<dim3(ga + gb), dim3(256), 0, st>>>(a, dA.ld, m, b, dB.ld, n, len, log2M, sftA, sftB, ga)
+#define OZ2_SP(r) launch(stats_pair_kernel<r>, dim3(ga + gb), dim3(256), st, a, dA.ld, m, b, dB.ld, n, len, log2M, sftA, sftB, ga)
     if (rows == 16) OZ2_SP(16);
     else if (rows == 8) OZ2_SP(8);
     else OZ2_SP(4);
@@ -848,8 +848,8 @@ template <typename R, bool CPLX, bool CA, bool CB>
 static void launch_encode_pair(const EncOperand &a, const EncOperand &b, const Layout &L, const ModParams &MP,
                                hipStream_t st) {
     const ModGroups G = make_groups(MP, L.N);
-    encode_pair_kernel<R, CPLX, CA, CB><<<dim3(a.gx * a.gy + b.gx * b.gy), dim3(CPLX ? 128 : 256), 0, st>>>(
-        a, b, L.ksteps, L.kblk, MP, G);
+    launch(encode_pair_kernel<R, CPLX, CA, CB>, dim3(a.gx * a.gy + b.gx * b.gy), dim3(CPLX ? 128 : 256), st, a, b,
+           L.ksteps, L.kblk, MP, G);
 }
 template <typename R, bool CPLX>
 static void launch_encode_pair_ops(bool ca, bool cb, const EncOperand &a, const EncOperand &b, const Layout &L,
@@ -899,8 +899,8 @@ bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, s
 
 void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
                              hipStream_t st, bool cplx_rows) {
-    finalize_accurate_sft_kernel<<<dim3((unsigned)((nvec + 255) / 256)), dim3(256), 0, st>>>(sft0, bound, nvec, log2M, out,
-                                                                                          cplx_rows ? 1 : 0);
+    launch(finalize_accurate_sft_kernel, dim3((unsigned)((nvec + 255) / 256)), dim3(256), st, sft0, bound, nvec, log2M,
+           out, cplx_rows ? 1 : 0);
 }
 
 }  // namespace oz2
