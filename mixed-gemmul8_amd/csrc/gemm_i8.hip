@@ -896,7 +896,7 @@ static unsigned device_cu_count() {
     return cached[dev];
 }
 // GEMMUL8_PERSISTENT: 0 = one-tile kernel only, 1 = persistent kernel wherever it applies, unset =
-// persistent when the launch has at least four tiles per CU.  g_persistent_override (probes) wins when >= 0.
+// persistent when the launch has at least three tiles per CU.  g_persistent_override (probes) wins when >= 0.
 int g_persistent_override = -1;
 int g_prio_override = 1;  // probes: the persistent kernel's priority variant (PRIO; 1 = the default)
 int g_epim_override = 0;  // probes: the persistent kernel's residue arithmetic (EPIM; 0 = the default)
@@ -911,7 +911,8 @@ static int persistent_mode() {
 }
 
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
-             int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue) {
+             int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue,
+             bool queue_zeroed) {
     GemmArgs g{};
     g.A = A8;
     g.B = B8;
@@ -968,17 +969,19 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         return;
     }
     // persistent residue kernel: a tile-queue area, buffer descriptors (planes < 4 GiB),
-    // >= 6 k-steps per tile (the kernel's cursor jump at k = K - 4 after its first two steps) and, by default, >= 4 tiles per CU (measured, same process: cfg2 products 5.16 -> 5.04 ms,
-    // 8192^2 x 1024 1.14 -> 1.01 ms, 4096^3 0.857 -> 0.842 ms; at 2048^3, 3.5 tiles per CU, the
-    // queue-zeroing launch costs more than the persistent kernel saves: 0.115 -> 0.118 ms)
+    // >= 6 k-steps per tile (the kernel's cursor jump at k = K - 4 after its first two steps) and, by
+    // default, >= 3 tiles per CU (measured, same process: cfg2 products 5.16 -> 5.04 ms, 8192^2 x 1024
+    // 1.14 -> 1.01 ms, 4096^3 0.857 -> 0.842 ms; with the queue zeroed by the encode instead of a launch
+    // of its own, tools/probes/persist_threshold.sh: 2048^3 (3.5 tiles per CU) 112.8 -> 110.3 us,
+    // 2560^3 199.1 -> 192.0 us, 3072^3 317.0 -> 305.7 us, but 1536^3 (2 per CU) 57.6 -> 65.2 us)
     const unsigned ntiles_all = (unsigned)(L.mtiles * L.ntiles) * nplanes * g.nsub;
     const unsigned ncu = device_cu_count();
     const int pmode = persistent_mode();
-    if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 4 * ncu)) {
+    if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 3 * ncu)) {
         g.nplanes = nplanes * g.nsub;
         g.queue = queue;
         g.stamps = g_stamps;
-        zero_i32(reinterpret_cast<int32_t *>(queue), 8, st);
+        if (!queue_zeroed) zero_i32(reinterpret_cast<int32_t *>(queue), 8, st);
         // GEMMUL8_PERSISTENT_GRID caps the grid (tests: many tiles per block at small shapes), at no fewer
         // than 8 blocks: every XCD queue that holds tiles needs a block of its own (bid mod 8)
         static const unsigned grid_cap = [] {

@@ -295,7 +295,8 @@ static void operand_shifts(const Call &c, const Views &v, bool is_A, hipStream_t
 static void operand_encode(const Call &c, const Views &v, bool is_A, unsigned j0, unsigned j1, unsigned slot,
                            hipStream_t st) {
     const Layout &L = v.L;
-    const ModParams SP = sub_mod_params(c.N, j0, j1);
+    ModParams SP = sub_mod_params(c.N, j0, j1);
+    SP.zero_queue = is_A ? v.queue : nullptr;  // the products that follow find their tile queue zeroed
     if (is_A) split_encode(c.A, true, c.m, c.k, v.sftA, v.A8 + slot * L.planeA, L.planeA, L, 0, SP, st);
     else split_encode(c.B, false, c.n, c.k, v.sftB, v.B8 + slot * L.planeB, L.planeB, L, 0, SP, st);
 }
@@ -314,8 +315,10 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
             operand_shifts(c, v, false, c.st);
         }
         const Layout &L = v.L;
+        ModParams SP = sub_mod_params(c.N, j0, j1);
+        SP.zero_queue = v.queue;
         if (split_encode_pair(c.A, c.m, c.B, c.n, c.k, v.sftA, v.sftB, v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB, L,
-                              sub_mod_params(c.N, j0, j1), c.st))
+                              SP, c.st))
             return;
         operand_encode(c, v, true, j0, j1, j0, c.st);
         operand_encode(c, v, false, j0, j1, j0, c.st);
@@ -330,11 +333,13 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
 }
 
 // phase 2: residue planes j0..j1-1 from the slice planes starting at `slot` (one launch;
-// conv_32i_2_8u fused into the epilogue)
-static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1, unsigned slot, hipStream_t st) {
+// conv_32i_2_8u fused into the epilogue).  queue_zeroed: the A encode just before on this stream
+// zeroed the tile queue (phase_split, operand_encode); otherwise the products zero it themselves.
+static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1, unsigned slot, hipStream_t st,
+                           bool queue_zeroed) {
     const Layout &L = v.L;
     gemm_i8(v.A8 + slot * L.planeA, v.B8 + slot * L.planeB, L, j1 - j0, Epi::RESIDUE, v.R + j0 * L.planeR, nullptr,
-            nullptr, sub_mod_params(N, j0, j1), st, v.queue);
+            nullptr, sub_mod_params(N, j0, j1), st, v.queue, queue_zeroed);
 }
 
 // phase 3: CRT + scaling + BLAS epilogue over all N residue planes
@@ -378,7 +383,7 @@ static int run(Call &c, double *phase_ns) {
         split.end();
         if (!launch_ok()) return fail();
         timing::Phase prod(record, c.st, rec.prod0, rec.prod1);
-        phase_products(v, c.N, 0, c.N, 0, c.st);
+        phase_products(v, c.N, 0, c.N, 0, c.st, true);
         prod.end();
         if (!launch_ok()) return fail();
     } else {
@@ -400,7 +405,7 @@ static int run(Call &c, double *phase_ns) {
             operand_encode(c, v, false, j0, j1, 0, c.stB);
             join(c);
             if (!launch_ok()) return fail();
-            phase_products(v, c.N, j0, j1, 0, c.st);
+            phase_products(v, c.N, j0, j1, 0, c.st, true);
             if (!launch_ok()) return fail();
         }
         prod.end();
@@ -567,7 +572,7 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
         }
     }
     oz2::timing::Phase prod(record, st, rec.prod0, rec.prod1);
-    oz2::phase_products(v, num_moduli, mod_begin, mod_end, mod_begin, st);
+    oz2::phase_products(v, num_moduli, mod_begin, mod_end, mod_begin, st, false);
     prod.end();
     if (record) {
         std::lock_guard<std::mutex> g(oz2::timing::mu);

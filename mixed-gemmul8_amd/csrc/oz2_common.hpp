@@ -166,6 +166,9 @@ struct ModParams {
     double rinv_d[OZ2_MAX_MODULI];
     float rinv_f[OZ2_MAX_MODULI];
     unsigned N;
+    // slice encodes only: the persistent product kernel's 8 tile-queue heads, zeroed by the encode's
+    // first block (the products follow the encode on the stream; saves a zeroing launch per call)
+    uint32_t *zero_queue;
 };
 
 static inline ModParams make_mod_params(unsigned N) {

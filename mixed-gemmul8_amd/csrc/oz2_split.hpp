@@ -76,9 +76,11 @@ enum class Epi : int { RESIDUE = 0, BOUND = 1, RAW = 2 };
 // Products of the N slice planes: residue planes (uint8, [N][n_pad][m_pad]),
 // bound (rowmax[m_pad], colmax[n_pad] of |C|, must be zeroed), or raw int32 (plane 0 only).
 // queue: the workspace's tile-queue area (Layout::offQueue) for the persistent residue kernel
-// (nullptr: one-tile kernel only).
+// (nullptr: one-tile kernel only); queue_zeroed: an earlier launch on st zeroed it (else a zeroing
+// launch precedes the persistent kernel).
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
-             int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue = nullptr);
+             int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue = nullptr,
+             bool queue_zeroed = false);
 // exhaustive exactness check of the residue epilogues (0 = biased, 1 = signed): mismatch count
 unsigned long long residue_selftest(int path, hipStream_t st);
 

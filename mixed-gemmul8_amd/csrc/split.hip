@@ -90,12 +90,17 @@ static ModGroups make_groups(const ModParams &MP, unsigned Ncall) {
     return G;
 }
 
-template <typename R> __device__ __forceinline__ R fma_ru(R a, R b, R c);
-template <> __device__ __forceinline__ double fma_ru<double>(double a, double b, double c) { return __fma_ru(a, b, c); }
-template <> __device__ __forceinline__ float fma_ru<float>(float a, float b, float c) { return __fmaf_ru(a, b, c); }
 template <typename R> __device__ __forceinline__ R add_ru(R a, R b);
 template <> __device__ __forceinline__ double add_ru<double>(double a, double b) { return __dadd_ru(a, b); }
 template <> __device__ __forceinline__ float add_ru<float>(float a, float b) { return __fadd_ru(a, b); }
+
+// loads in flight per thread in the stats passes (probe builds vary them: tools/probes/stats_probe.hip)
+#ifndef OZ2_STRIDED_LOADS
+#define OZ2_STRIDED_LOADS 16
+#endif
+#ifndef OZ2_CONTIG_LOADS
+#define OZ2_CONTIG_LOADS 8
+#endif
 
 // reference wave tree: __shfl_down width 64, steps 16..1 (inner_warp_sum on wave64)
 template <typename R> __device__ __forceinline__ R ref_wave_sum(R v) {
@@ -134,17 +139,45 @@ __device__ __forceinline__ void load_elem(const R *__restrict__ X, size_t idx, R
     }
 }
 
-template <typename R, bool CPLX>
+// s + x*x rounded upward (the reference's __fma_ru on the sum of squares, scaling.hpp:155-213) as
+// inline code: the OCML helper behind __fma_ru is a call whose entry waits for every memory access
+// in flight (s_waitcnt 0), which held each load of the stats passes behind the previous element's
+// fma.  Same instruction, same rounding mode switch: FP64 round bits MODE[3:2], FP32 MODE[1:0],
+// 1 = toward +inf, restored to 0 (nearest even, the kernels' mode) after one wait state.
+template <typename R> __device__ __forceinline__ R sq_add_ru(R x, R s);
+template <> __device__ __forceinline__ double sq_add_ru<double>(double x, double s) {
+    asm("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 1\n\t"
+        "v_fma_f64 %0, %1, %1, %0\n\t"
+        "s_nop 0\n\t"
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0"
+        : "+v"(s)
+        : "v"(x));
+    return s;
+}
+template <> __device__ __forceinline__ float sq_add_ru<float>(float x, float s) {
+    asm("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 2), 1\n\t"
+        "v_fma_f32 %0, %1, %1, %0\n\t"
+        "s_nop 0\n\t"
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 0, 2), 0"
+        : "+v"(s)
+        : "v"(x));
+    return s;
+}
+
+// SUM = false: the accurate-mode pass, which needs amax only
+template <typename R, bool CPLX, bool SUM = true>
 __device__ __forceinline__ void accum(R re, R im, R &amax, R &sum) {
     re = fabs(re);
     if constexpr (CPLX) {
         im = fabs(im);
         amax = fmax(amax, fmax(re, im));
-        sum = fma_ru<R>(re, re, sum);
-        sum = fma_ru<R>(im, im, sum);
+        if (SUM) {
+            sum = sq_add_ru<R>(re, sum);
+            sum = sq_add_ru<R>(im, sum);
+        }
     } else {
         amax = fmax(amax, re);
-        sum = fma_ru<R>(re, re, sum);
+        if (SUM) sum = sq_add_ru<R>(re, sum);
     }
 }
 
@@ -163,19 +196,19 @@ __device__ __forceinline__ void stats_contig_body(const R *__restrict__ X, size_
     R amax = 0, sum = 0;
     // loads are issued in unguarded batches of U ahead of the round-up chain (whose
     // mode-register writes would otherwise serialise each load behind the previous fma)
-    constexpr int U = 8;
+    constexpr int U = OZ2_CONTIG_LOADS;
     size_t e = t;
     for (; e + (U - 1) * VT < len; e += U * VT) {
         R re[U], im[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) load_elem<R, CPLX>(x, e + u * VT, re[u], im[u]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) accum<R, CPLX>(re[u], im[u], amax, sum);
+        for (int u = 0; u < U; ++u) accum<R, CPLX, !ACCU>(re[u], im[u], amax, sum);
     }
     for (; e < len; e += VT) {
         R re, im;
         load_elem<R, CPLX>(x, e, re, im);
-        accum<R, CPLX>(re, im, amax, sum);
+        accum<R, CPLX, !ACCU>(re, im, amax, sum);
     }
     amax = wave_max<R>(amax);
     if (!ACCU) {
@@ -226,7 +259,8 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
                                                    StridedShared<R, VT, ROWS> &sh) {
     constexpr int SLOTS = 256 / ROWS;
     constexpr int NA = VT / SLOTS;
-    constexpr int U = (ROWS == 16 || NA >= 16) ? 1 : 16 / NA;  // batching measured slower at 16 rows
+    // loads in flight per thread: U * NA (OZ2_STRIDED_LOADS; probe builds vary it)
+    constexpr int U = NA >= OZ2_STRIDED_LOADS ? 1 : OZ2_STRIDED_LOADS / NA;
     static_assert(SLOTS <= 64 && NA >= 1, "one reduction lane per slot");
     auto &part = sh.part;
     auto &pmax = sh.pmax;
@@ -248,14 +282,14 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int c = 0; c < NA; ++c) accum<R, CPLX>(re[u][c], im[u][c], amax, acc[c]);
+                for (int c = 0; c < NA; ++c) accum<R, CPLX, !ACCU>(re[u][c], im[u][c], amax, acc[c]);
         }
         for (; b + VT <= len; b += VT) {
             R re[NA], im[NA];
 #pragma unroll
             for (int c = 0; c < NA; ++c) load_elem<R, CPLX>(X, (b + slot + SLOTS * c) * ld + v, re[c], im[c]);
 #pragma unroll
-            for (int c = 0; c < NA; ++c) accum<R, CPLX>(re[c], im[c], amax, acc[c]);
+            for (int c = 0; c < NA; ++c) accum<R, CPLX, !ACCU>(re[c], im[c], amax, acc[c]);
         }
         for (; b < len; b += VT) {
 #pragma unroll
@@ -264,7 +298,7 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
                 if (e < len) {
                     R re, im;
                     load_elem<R, CPLX>(X, e * ld + v, re, im);
-                    accum<R, CPLX>(re, im, amax, acc[c]);
+                    accum<R, CPLX, !ACCU>(re, im, amax, acc[c]);
                 }
             }
         }
@@ -690,6 +724,7 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                                                                    size_t ksteps, size_t kblk, size_t vmax,
                                                                    int flags, ModParams MP, ModGroups G) {
     __shared__ EncTile<R, CPLX> tile;
+    if (MP.zero_queue && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
     encode_body<R, CPLX, CONTIG, IS_A, MODE>(X, ld, nvec, len, sft, out, plane, ksteps, kblk, vmax, flags, MP, G,
                                              blockIdx.x, blockIdx.y, tile);
 }
@@ -710,6 +745,7 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_pair_kernel(EncOperan
                                                                         size_t kblk, ModParams MP, ModGroups G) {
     __shared__ EncTile<R, CPLX> tile;
     const unsigned na = a.gx * a.gy;
+    if (MP.zero_queue && blockIdx.x == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
     if (blockIdx.x < na) {
         encode_body<R, CPLX, CONTIG_A, true, 0>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.sft, a.out, a.plane,
                                                 ksteps, kblk, a.vmax, a.flags, MP, G, blockIdx.x % a.gx, blockIdx.x / a.gx,

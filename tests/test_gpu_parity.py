@@ -607,10 +607,11 @@ def test_persistent_products_forced():
 
 
 def test_persistent_default_matches_one_tile():
-    """Production shapes where the default rule picks the persistent residue kernel (>= 4 tiles per
+    """Production shapes where the default rule picks the persistent residue kernel (>= 3 tiles per
     CU): C bit-identical to the one-tile kernel (GEMMUL8_PERSISTENT=0, child process) at k-steps per
-    tile around the kernel's minimum (5: one-tile kernel; 6, 7, 128: persistent).  With 5 k-steps
-    the persistent kernel's DMA cursor used to jump to the next tile before it was decoded."""
+    tile around the kernel's minimum (5: one-tile kernel; 6, 7, 128: persistent), and at 2048^3
+    (3.5 tiles per CU: blocks with different tile counts).  With 5 k-steps the persistent kernel's
+    DMA cursor used to jump to the next tile before it was decoded."""
     import subprocess
     import tempfile
     tdir = os.path.dirname(os.path.abspath(__file__))
@@ -618,15 +619,15 @@ def test_persistent_default_matches_one_tile():
     code = ("import sys, numpy as np, torch; sys.path[:0] = sys.argv[1:3]\n"
             "import gemmul8 as G\n"
             "out = sys.argv[3]; res = {}\n"
-            "for k in (300, 330, 400, 8192):\n"
-            "    m = n = 4096\n"
+            "for m, k in ((4096, 300), (4096, 330), (4096, 400), (4096, 8192), (2048, 2048)):\n"
+            "    n = m\n"
             "    g = torch.Generator(device='cuda'); g.manual_seed(k)\n"
             "    A = torch.randn((k, m), dtype=torch.float64, device='cuda', generator=g)\n"
             "    B = torch.randn((n, k), dtype=torch.float64, device='cuda', generator=g)\n"
             "    C = torch.empty((n, m), dtype=torch.float64, device='cuda')\n"
             "    W = G.alloc_work(m, n, k, 14)\n"
             "    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C, m, 14, True, W)\n"
-            "    res[str(k)] = C.cpu().numpy()\n"
+            "    res[f'{m}_{k}'] = C.cpu().numpy()\n"
             "np.savez(out, **res)\n")
     with tempfile.TemporaryDirectory() as d:
         outs = []
