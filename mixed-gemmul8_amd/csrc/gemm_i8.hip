@@ -549,6 +549,8 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
 // the blocks drift apart over the launch and the L2 hit rate fell from 79 % to 69 %.)  The first
 // tile of a block is its slot on the XCD, the second is dequeued at the start, every later one in
 // the epilogue two tiles ahead, so the DMA cursor always knows the tile it runs into.
+constexpr int PSTAGES = 4;                   // the persistent kernel's ring (its vmcnt bookkeeping assumes 4)
+constexpr int PLDS_BYTES = PSTAGES * SLOT;
 constexpr int PARK_SPARE = 32768;
 constexpr int PARK_STORES = 4096 / NTHREADS;  // 16-byte residue stores per thread (and per wave) per tile
 constexpr unsigned NO_TILE = 0xffffffffu;
@@ -612,13 +614,13 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
     do {                \
     } while (0)
 #endif
-    __shared__ __attribute__((aligned(1024))) int8_t smem[LDS_BYTES + PARK_SPARE];
-    static_assert(LDS_BYTES + PARK_SPARE <= 160 * 1024, "LDS");
-    static_assert(STAGES == 4 && GLDS_PER_STEP == 4 && PARK_STORES == 8, "vmcnt bookkeeping below assumes these");
+    __shared__ __attribute__((aligned(1024))) int8_t smem[PLDS_BYTES + PARK_SPARE];
+    static_assert(PLDS_BYTES + PARK_SPARE <= 160 * 1024, "LDS");
+    static_assert(PSTAGES == 4 && GLDS_PER_STEP == 4 && PARK_STORES == 8, "vmcnt bookkeeping below assumes these");
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = wave >> 2, wc = wave & 3;
-    uint32_t *const spare = reinterpret_cast<uint32_t *>(smem + LDS_BYTES);
+    uint32_t *const spare = reinterpret_cast<uint32_t *>(smem + PLDS_BYTES);
     if (PRIO == 1 && wr == 1) __builtin_amdgcn_s_setprio(1);
 
     // this block's XCD queue: the XCD's share of every plane (the one-tile kernel's remap)
@@ -651,12 +653,12 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
     // may exceed it): the DMA switches to the successor tile's descriptors with its cursor
     auto rsrcA = [&](const TileRef &t) { return make_rsrc(g.A + (size_t)t.j * g.planeA, (uint32_t)g.planeA); };
     auto rsrcB = [&](const TileRef &t) { return make_rsrc(g.B + (size_t)t.j * g.planeB, (uint32_t)g.planeB); };
-    auto lo_of = [&](unsigned step) { return lds_wave + (step & (STAGES - 1)) * SLOT; };
-    auto rd_of = [&](unsigned step) { return smem + (step & (STAGES - 1)) * SLOT; };
+    auto lo_of = [&](unsigned step) { return lds_wave + (step & (PSTAGES - 1)) * SLOT; };
+    auto rd_of = [&](unsigned step) { return smem + (step & (PSTAGES - 1)) * SLOT; };
 
     TileRef ct = decode_tile<SUB>(g, tile_u(ccur));
     v4si rA = rsrcA(ct), rB = rsrcB(ct);  // descriptors of the DMA cursor
-    constexpr unsigned D = STAGES - 1;
+    constexpr unsigned D = PSTAGES - 1;
     for (unsigned s0 = 0; s0 < D; ++s0) {  // steps 0..2 of the first tile
         const uint32_t lo = lo_of(s0);
         bglds16(rA, ct.offA + s0 * PANEL + lane_off, lo);

@@ -20,8 +20,9 @@ __global__ void empty_kernel() {}
 
 int main() {
     const unsigned N = 14;
-    for (size_t k : {64, 1024}) {
-        const size_t m = 1024, n = 1024;
+    const size_t shapes[][2] = {{1024, 64}, {1024, 1024}, {1024, 4096}, {2048, 2048}, {1536, 1536}};
+    for (auto &sh : shapes) {
+        const size_t m = sh[0], n = sh[0], k = sh[1];
         oz2::Layout L = oz2::make_layout(m, n, k, N, false);
         void *w;
         if (hipMalloc(&w, L.total) != hipSuccess) return 1;
@@ -52,7 +53,7 @@ int main() {
             (void)hipEventElapsedTime(&s, e0, e1);
             single += s / 20;
         }
-        printf("ablate=%d m=n=1024 k=%4zu N=14: back-to-back %.2f us/launch, single %.2f us\n", OZ2_ABLATE, k,
+        printf("stages=%d ablate=%d m=n=%zu k=%4zu N=14: back-to-back %.2f us/launch, single %.2f us\n", OZ2_STAGES, OZ2_ABLATE, m, k,
                ms * 1e3 / R, single * 1e3);
         (void)hipFree(w);
     }
