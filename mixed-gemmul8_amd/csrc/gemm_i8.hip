@@ -178,6 +178,22 @@ __device__ __forceinline__ uint32_t residue_biased_f64(uint32_t u, double invp, 
     return (uint32_t)__double2loint(__builtin_fma(q, pneg, zc));
 }
 
+// Two forms without v_floor_f64 (A/B probes, EPIM 3 / 4).  y = fma(zc, fl(1/p), c - 1/2) is u/p + 2^-8 - 1/2
+// within 2^-28 (c - 1/2 stays exact: a multiple of 2^-8 below 2^45), i.e. q + f with |f| < 1/2 strictly
+// (r/p + 2^-8 <= 254/255 + 2^-8 < 1 for p <= 255), so t = y + 1.5 * 2^52 rounds to 1.5 * 2^52 + q exactly and
+// the low dword of t is q = floor(u/p).  EPIM 3 finishes in f64 (q = t - 1.5 * 2^52, fma back), EPIM 4 in
+// 32-bit integers (r = u - q p, q < 2^24).
+__device__ __forceinline__ uint32_t residue_biased_f64r(uint32_t u, double invp, double chalf, double pneg) {
+    const double zc = __hiloint2double(0x43300000, (int)u);
+    const double t = __builtin_fma(zc, invp, chalf) + 0x1.8p52;
+    return (uint32_t)__double2loint(__builtin_fma(t - 0x1.8p52, pneg, zc));
+}
+__device__ __forceinline__ uint32_t residue_biased_f64i(uint32_t u, double invp, double chalf, uint32_t p) {
+    const double zc = __hiloint2double(0x43300000, (int)u);
+    const double t = __builtin_fma(zc, invp, chalf) + 0x1.8p52;
+    return u - __umul24((uint32_t)__double2loint(t), p);
+}
+
 // four residues in [0, p) per word: (a + b) mod p bytewise
 __device__ __forceinline__ uint32_t add_mod_bytes(uint32_t a, uint32_t b, uint32_t p) {
     uint32_t r = 0;
@@ -781,6 +797,14 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             const double invp = g.invp[ct.j], pneg = -(double)p;
             const double cneg = __builtin_fma(-0x1p52, invp, 0x1p-8);
             park([&](int x) { return residue_biased_f64((uint32_t)x, invp, cneg, pneg); });
+        } else if (EPIM == 3 && g.biased) {
+            const double invp = g.invp[ct.j], pneg = -(double)p;
+            const double chalf = __builtin_fma(-0x1p52, invp, 0x1p-8) - 0.5;
+            park([&](int x) { return residue_biased_f64r((uint32_t)x, invp, chalf, pneg); });
+        } else if (EPIM == 4 && g.biased) {
+            const double invp = g.invp[ct.j];
+            const double chalf = __builtin_fma(-0x1p52, invp, 0x1p-8) - 0.5;
+            park([&](int x) { return residue_biased_f64i((uint32_t)x, invp, chalf, (uint32_t)p); });
         } else if (g.biased) {
             const uint32_t m = g.minv[ct.j];
             park([&](int x) { return residue_biased((uint32_t)x, (uint32_t)p, m); });
@@ -994,6 +1018,10 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 1) launch(gemm_i8_persistent_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 2) launch(gemm_i8_persistent_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
+#ifdef OZ2_EPIM_PROBES
+        else if (g_epim_override == 3) launch(gemm_i8_persistent_kernel<false, 1, 3>, pgrid, dim3(NTHREADS), st, g);
+        else if (g_epim_override == 4) launch(gemm_i8_persistent_kernel<false, 1, 4>, pgrid, dim3(NTHREADS), st, g);
+#endif
         else if (g_prio_override == 0) launch(gemm_i8_persistent_kernel<false, 0>, pgrid, dim3(NTHREADS), st, g);
         else if (g_prio_override == 2) launch(gemm_i8_persistent_kernel<false, 2>, pgrid, dim3(NTHREADS), st, g);
         else launch(gemm_i8_persistent_kernel<false, 1>, pgrid, dim3(NTHREADS), st, g);

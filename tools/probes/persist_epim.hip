@@ -2,6 +2,7 @@
 // rounds, random operand bytes): EPIM 0 (f64 form, the default), 1 (low byte only: wrong residues,
 // the cost of the reduction), 2 (integer biased Barrett, the earlier default); cfg2-shaped launches
 // (m = n = 8192, N planes, k from argv[2]); checks that variants 0 and 2 write identical residues.
+#define OZ2_EPIM_PROBES 1
 #include "../../mixed-gemmul8_amd/csrc/gemm_i8.hip"
 #include <cstdio>
 #include <cstring>
@@ -35,9 +36,9 @@ int main(int argc, char **argv) {
     oz2::ModParams MP = oz2::make_mod_params(N);
     int8_t *b = (int8_t *)w;
     const size_t rbytes = (size_t)N * L.planeR;
-    constexpr int NV = 3;
+    constexpr int NV = 5;
     uint8_t *R2[NV];
-    for (int v = 0; v < 3; ++v)
+    for (int v = 0; v < NV; ++v)
         if (hipMalloc(&R2[v], rbytes) != hipSuccess) return 1;
     uint32_t *queue = reinterpret_cast<uint32_t *>(b + L.offQueue);
     std::vector<float> t[NV];
@@ -60,13 +61,15 @@ int main(int argc, char **argv) {
     std::vector<uint8_t> h1(rbytes), h2(rbytes);
     bool same = true;
     (void)hipMemcpy(h1.data(), R2[0], rbytes, hipMemcpyDeviceToHost);
-    (void)hipMemcpy(h2.data(), R2[2], rbytes, hipMemcpyDeviceToHost);
-    same = memcmp(h1.data(), h2.data(), rbytes) == 0;
+    for (int v : {2, 3, 4}) {
+        (void)hipMemcpy(h2.data(), R2[v], rbytes, hipMemcpyDeviceToHost);
+        same = same && memcmp(h1.data(), h2.data(), rbytes) == 0;
+    }
     for (int v = 0; v < NV; ++v) {
         std::sort(t[v].begin(), t[v].end());
-        printf("%s N=%u m=%zu n=%zu k=%zu: median %.3f ms min %.3f ms  %.0f TOPS\n", v == 0 ? "f64 residue" : v == 1 ? "low byte   " : "int residue", N,
+        printf("%s N=%u m=%zu n=%zu k=%zu: median %.3f ms min %.3f ms  %.0f TOPS\n", v == 0 ? "f64 floor  " : v == 1 ? "low byte   " : v == 2 ? "int residue" : v == 3 ? "f64 round  " : "f64+int    ", N,
                m, n, k, t[v][t[v].size() / 2], t[v][0], 2.0 * m * n * L.k_pad * N / t[v][t[v].size() / 2] / 1e9);
     }
-    printf("residues identical (f64 vs int): %s\n", same ? "yes" : "NO");
+    printf("residues identical (forms 0, 2, 3, 4): %s\n", same ? "yes" : "NO");
     return same ? 0 : 3;
 }
