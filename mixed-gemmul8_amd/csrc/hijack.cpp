@@ -22,7 +22,8 @@
 // would apply beta to a C the emulator may already have written): it returns an execution error.
 //
 // Workspaces: an eager call uses one buffer per (device, stream), grown on demand (calls on one
-// stream are ordered, so reuse is safe).  A call captured into a graph never uses that buffer (a
+// stream are ordered, so reuse is safe; the lookup and the call's enqueue happen under one lock, so
+// a call of another thread on the same stream cannot free the buffer between them).  A call captured into a graph never uses that buffer (a
 // later, larger eager call would free it under the graph, and graphs captured on one stream would
 // share it and race when replayed on different streams): each (device, capture, stream) gets a
 // buffer of its own, allocated during the capture under relaxed capture mode and never freed,
@@ -175,9 +176,14 @@ const Config &cfg() {
 
 std::atomic<void *> last_workspace{nullptr};  // test hook: gemmul8_hijack_last_workspace()
 
-// workspace of one call (see the header comment); nullptr: none available, forward the call
+// held from the workspace lookup until the call using it is enqueued: growing a stream's eager
+// buffer frees the old one (after a stream sync), which must not happen between another thread's
+// lookup and its enqueue on the same stream
+std::mutex ws_mu;
+
+// workspace of one call (see the header comment); nullptr: none available, forward the call.
+// The caller holds ws_mu.
 void *workspace(size_t bytes, hipStream_t st) {
-    static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, std::pair<void *, size_t>> eager;
     // (device, capture id, stream) -> the capture's current buffer; every buffer ever handed to a
     // capture stays allocated (the graph's nodes hold its address)
@@ -192,7 +198,6 @@ void *workspace(size_t bytes, hipStream_t st) {
     } else if (a.isCapturing && a.isCapturing(st, &cap) != hipSuccess) {
         return nullptr;
     }
-    std::lock_guard<std::mutex> g(mu);
     if (cap != hipStreamCaptureStatusNone) {
         if (cap != hipStreamCaptureStatusActive || !a.captureInfo || !a.exchangeCaptureMode) return nullptr;
         auto &e = captured[{dev, id, st}];
@@ -236,11 +241,15 @@ Outcome emulate(const char *fn, const Mode &md, hipStream_t st, int opa, int opb
     const bool cplx = type == GEMMUL8_C_64F || type == GEMMUL8_C_32F;
     const int ct = cplx ? c.ctype : GEMMUL8_REAL_DEFAULT;
     const size_t ws = api().workSize(m, n, k, md.N, ct);
-    void *work = ws ? workspace(ws, st) : nullptr;
-    if (!work) return Outcome::forward;
-    last_workspace.store(work);
-    const int rc = api().gemm(st, op_code(opa), op_code(opb), m, n, k, type, type, type, alpha, A, lda, B, ldb, beta,
-                                C, ldc, md.N, md.fast, work, ct, nullptr);
+    int rc;
+    {
+        std::lock_guard<std::mutex> g(ws_mu);
+        void *work = ws ? workspace(ws, st) : nullptr;
+        if (!work) return Outcome::forward;
+        last_workspace.store(work);
+        rc = api().gemm(st, op_code(opa), op_code(opb), m, n, k, type, type, type, alpha, A, lda, B, ldb, beta, C, ldc,
+                        md.N, md.fast, work, ct, nullptr);
+    }
     const Outcome o = rc == GEMMUL8_OK ? Outcome::emulated : (rc == GEMMUL8_E_HIP ? Outcome::failed : Outcome::forward);
     if (c.info)
         fprintf(stderr, "[gemmul8] %s m=%ld n=%ld k=%ld -> %s (num_moduli=%u, %s)\n", fn, m, n, k,

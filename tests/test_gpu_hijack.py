@@ -7,7 +7,8 @@ of the capture's own (never the stream's eager buffer): a later, larger eager ca
 stream must not pull it from under the graph, and two graphs captured on one stream must replay
 concurrently on two streams without sharing it.  A HIP error left pending by the application before
 an interposed DGEMM with beta != 0 must not make the call look failed (which used to forward it to
-the vendor routine after the emulator had written C, applying beta twice)."""
+the vendor routine after the emulator had written C, applying beta twice).  Two threads on one stream
+with growing sizes must get the emulator's bits (a growing call frees the stream's eager buffer)."""
 import json
 import os
 import subprocess
@@ -130,6 +131,26 @@ for _ in range(4):
     ok = ok and bool(torch.equal(Cx, Ex)) and bool(torch.equal(Cy, Ey))
 out["concurrent_replays_bits"] = ok
 
+# two threads on the one default stream, sizes growing: each growth frees the stream's eager buffer,
+# which must not happen between the other thread's workspace lookup and its enqueue
+import threading
+res_t = []
+def worker(seed):
+    gg = torch.Generator(device="cuda").manual_seed(seed)
+    ok = True
+    for m in (256, 384, 640, 896, 1152, 1408, 1664):
+        A = torch.randn(m, m - 64, dtype=torch.float64, device="cuda", generator=gg)
+        B = torch.randn(m - 64, m + 32, dtype=torch.float64, device="cuda", generator=gg)
+        C = torch.matmul(A, B)
+        ok = ok and bool(torch.equal(C, emu(A, B)))
+    res_t.append(ok)
+ths = [threading.Thread(target=worker, args=(100 + i,)) for i in range(2)]
+for t in ths:
+    t.start()
+for t in ths:
+    t.join()
+out["threads_same_stream_bits"] = len(res_t) == 2 and all(res_t)
+
 # a HIP error left pending by the application, then an interposed DGEMM with beta = 0.5
 hip = ctypes.CDLL("libamdhip64.so.7", mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
 A5, B5 = mats(512, 448, 384)
@@ -180,6 +201,7 @@ def test_torch_matmul_is_emulated():
     assert res["capture_own_ws"], res
     assert res["graph_after_grow_bits"], res
     assert res["concurrent_replays_bits"], res
+    assert res["threads_same_stream_bits"], res
     assert res["stale_set"], res
     assert res.get("stale_beta_bits"), res
     assert "launch failed" not in log, log[-2000:]
