@@ -60,6 +60,16 @@ for s in sizes:
         g.replay()
     torch.cuda.synchronize()
     res["graph"] = (time.perf_counter() - t0) / REPS * 1e6
-    print(f"{s}: eager {res['eager'][0]:.1f} us/call (host issue {res['eager'][1]:.1f}), with events "
+    At, Bt = A.t(), B.t()  # logical m x k, k x n views for rocBLAS DGEMM
+    for _ in range(5):
+        torch.matmul(At, Bt)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(REPS):
+        torch.matmul(At, Bt)
+    torch.cuda.synchronize()
+    res["dgemm"] = (time.perf_counter() - t0) / REPS * 1e6
+    print(f"{s}: rocBLAS DGEMM {res['dgemm']:.1f} us/call ({2 * s**3 / res['dgemm'] / 1e6:.1f} TF), "
+          f"eager {res['eager'][0]:.1f} us/call ({2 * s**3 / res['eager'][0] / 1e6:.1f} TF; host issue {res['eager'][1]:.1f}), with events "
           f"{res['events'][0]:.1f} (issue {res['events'][1]:.1f}), phases {res['phases_us']}, graph {res['graph']:.1f} us/call",
           flush=True)
