@@ -196,6 +196,16 @@ __device__ __forceinline__ void kara_words(const uint64_t (&w1)[N], const uint64
 // one) is fully coalesced.  The BLAS epilogue runs after the transpose, on the
 // coalesced C read when beta != 0.  KARA (complex outputs): the residues of the real and
 // imaginary parts come from the three Karatsuba sub-planes instead of rows r and r + m.
+// LDS slot of row e of lane l in a wave's transpose buffer: l * 8 + (e ^ sw(l)), with sw(l) a multiple of
+// EPV (so the EPV consecutive rows of one 16-byte read stay adjacent and in order) that differs between
+// the lanes whose 8-row groups share a 256-byte LDS row; unswizzled, the 8-byte (f64) writes of a wave
+// hit the same banks 16 ways (complex f64: 32 ways), swizzled 4 ways
+template <typename E> __device__ __forceinline__ int crt_slot(int l, int e) {
+    constexpr int EPV = 16 / sizeof(E);
+    constexpr int SH = sizeof(E) == 4 ? 3 : sizeof(E) == 8 ? 2 : 1;  // log2 of the lanes per 256-byte row
+    return l * CRT_ROWS + (e ^ ((EPV * (l >> SH)) & (CRT_ROWS - 1)));
+}
+
 template <int OT, bool NUMM1, unsigned N, bool KARA = false>
 __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     using E = typename OutElem<OT>::T;
@@ -235,15 +245,15 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
                 const int sft = (int)sa[e] + sB;
                 const double vr = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}), sft);
                 if constexpr (OT == 0) {
-                    wb[lane * CRT_ROWS + e] = vr;
+                    wb[crt_slot<E>(lane, e)] = vr;
                 } else if constexpr (OT == 1) {
-                    wb[lane * CRT_ROWS + e] = __double2float_rn(vr);
+                    wb[crt_slot<E>(lane, e)] = __double2float_rn(vr);
                 } else {
 #pragma unroll
                     for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(wi[i] >> (8 * e));
                     const double vi = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}), sft);
-                    if constexpr (OT == 2) wb[lane * CRT_ROWS + e] = make_double2(vr, vi);
-                    else wb[lane * CRT_ROWS + e] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
+                    if constexpr (OT == 2) wb[crt_slot<E>(lane, e)] = make_double2(vr, vi);
+                    else wb[crt_slot<E>(lane, e)] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
                 }
             }
         }
@@ -254,7 +264,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
         for (int j = 0; j < CRT_ROWS / EPV; ++j) {
             const int idx = j * 64 * EPV + lane * EPV;
             E v[EPV];
-            *reinterpret_cast<int4 *>(v) = *reinterpret_cast<const int4 *>(wb + idx);
+            *reinterpret_cast<int4 *>(v) = *reinterpret_cast<const int4 *>(wb + crt_slot<E>(idx / CRT_ROWS, idx % CRT_ROWS));
             if (vec_ok && wrow0 + idx + EPV <= a.m) {
                 if (!plain_ab) {
                     E c[EPV];
