@@ -351,6 +351,26 @@ def test_k_beyond_int32_range_chunked():
     check_full(randmat_np(rng, 5, 70000, dtype=np.complex128), randmat_np(rng, 70000, 6, dtype=np.complex128), 12)
 
 
+def test_k_at_the_largest_accepted_size():
+    """the largest k a call accepts (padded k of the int8 product = 2^22, fast mode): the strided encode's
+    grid then has 65536 k-tiles in y, the device's limit (hipDeviceAttributeMaxGridDimY); real (k = 2^22)
+    and complex (k = 2^21: the big-matrix product's k is 2^22, the complex encode's k-tiles are 32 wide);
+    64 k-chunks of the residue product; and one more k-step is rejected before anything is launched"""
+    import torch
+    import gemmul8 as G
+    rng = np.random.default_rng(3)
+    check_full(randmat_np(rng, 3, 1 << 22), randmat_np(rng, 1 << 22, 5), 2)
+    check_full(randmat_np(rng, 2, 1 << 21, dtype=np.complex128), randmat_np(rng, 1 << 21, 3, dtype=np.complex128), 2,
+               ctype=1)
+    k = (1 << 22) + 1
+    A = torch.zeros((k, 3), dtype=torch.float64, device="cuda")
+    B = torch.zeros((5, k), dtype=torch.float64, device="cuda")
+    C = torch.zeros((5, 3), dtype=torch.float64, device="cuda")
+    W = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    with pytest.raises(G.Gemmul8Error):
+        G.gemm(0, 0, 3, 5, k, 1.0, A, 3, B, k, 0.0, C, 3, 2, True, W)
+
+
 @pytest.mark.parametrize("fast", [True, False])
 def test_k_chunks_forced(fast):
     """the chunked product forced at small k (GEMMUL8_KCHUNK: chunks of 2 k-steps in a child
