@@ -822,7 +822,11 @@ static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, si
     constexpr int NT = CPLX ? 128 : 256;
     if (L.kblk == 0 || vpad_grid == 0) return;  // k = 0: the slice planes are empty
     const R *x = static_cast<const R *>(X);
-    const bool kf = contig;  // k-first block order for contiguous vectors (-4.5 % on B, see encode_kernel)
+    // k-first block order for contiguous vectors (-4.5 % on B, see encode_body), unless the vector tiles
+    // would exceed the grid's reported y limit (hipDeviceAttributeMaxGridDimY = 65536: more than 4 Mi
+    // vectors; a 65540-tile launch still ran on MI355X, but nothing documents more); the k-tiles never do
+    // (k <= 2^22)
+    const bool kf = contig && vpad_grid / 64 <= 65536;
     if (kf) flags |= ENC_KFIRST;
     const dim3 grid = kf ? dim3((unsigned)(L.kblk / KT), (unsigned)(vpad_grid / 64))
                          : dim3((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));

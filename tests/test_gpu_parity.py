@@ -372,6 +372,30 @@ def test_k_at_the_largest_accepted_size():
 
 
 @pytest.mark.parametrize("fast", [True, False])
+def test_more_contiguous_vectors_than_grid_rows(fast):
+    """B with more than 4 Mi columns (op N: contiguous vectors; their 64-vector tiles exceed the grid's
+    y limit of 65536 in the k-first encode order, so the encode walks them in x): C against the oracle,
+    bit for bit (k = 64, 2 moduli; fast mode takes the one-launch pair encode, accurate mode the
+    per-operand encodes and the bound product).  The reference launches its column kernel with n
+    blocks in x (scaling.hpp:3731-3733)."""
+    import torch
+    import gemmul8 as G
+    from oracle import oracle as O
+    m, n, k, N = 3, (1 << 22) + 200, 64, 2
+    rng = np.random.default_rng(11)
+    A = randmat_np(rng, m, k)
+    B = randmat_np(rng, k, n)
+    dA = torch.from_numpy(np.ascontiguousarray(A.T)).cuda()
+    dB = torch.from_numpy(np.ascontiguousarray(B.T)).cuda()
+    dC = torch.zeros((n, m), dtype=torch.float64, device="cuda")
+    W = G.alloc_work(m, n, k, N)
+    G.gemm(0, 0, m, n, k, 1.0, dA, m, dB, k, 0.0, dC, m, N, fast, W)
+    torch.cuda.synchronize()
+    Co = np.asfortranarray(O.gemm(A, B, N, fast))
+    assert np.asfortranarray(dC.cpu().numpy().T).tobytes() == Co.tobytes()
+
+
+@pytest.mark.parametrize("fast", [True, False])
 def test_k_chunks_forced(fast):
     """the chunked product forced at small k (GEMMUL8_KCHUNK: chunks of 2 k-steps in a child
     process) gives the same bits as one pass"""
