@@ -1,5 +1,5 @@
-// hijack.cpp -- LD_PRELOAD interception of hipBLAS / rocBLAS {D,Z,S,C}GEMM, routed to the
-// emulator (the caller side of the path).  An unmodified application --
+// hijack.cpp -- LD_PRELOAD interception of hipBLAS / rocBLAS {D,Z,S,C}GEMM (plain, strided batched
+// and the Ex forms), routed to the emulator (the caller side of the path).  An unmodified application --
 // PyTorch's torch.matmul on float64 tensors calls hipblasDgemm -- runs its DGEMMs as Ozaki-II
 // int8 products:
 //
@@ -17,7 +17,12 @@
 //   GEMMUL8_INTERCEPT_THRESHOLD_M / _N / _K   emulate only when m, n, k are all >= (default 128)
 //   GEMMUL8_INFO=1                one line per call on stderr
 // Calls with device-resident alpha/beta (pointer mode device), sizes below the thresholds or
-// arguments the emulator rejects (nothing enqueued) go to the vendor routine unchanged.  A call
+// arguments the emulator rejects (nothing enqueued) go to the vendor routine unchanged.  The Ex forms
+// (hipblasGemmEx, hipblasGemmStridedBatchedEx, rocblas_gemm_ex, rocblas_gemm_strided_batched_ex) are
+// emulated when A, B and C share one of the four types and the compute type is that precision "at
+// least" (HIPBLAS_COMPUTE_64F / _32F; rocBLAS: the same datatype); pedantic compute types, mixed types
+// and rocBLAS calls whose output D is not C in place are forwarded (the reference's companion
+// interposer hooks cublasGemmEx and cublasGemmStridedBatchedEx the same way, ozIMMU_EF/src/cublas.cu:135, 318).  A call
 // whose kernels were enqueued and then failed to launch is never forwarded (the vendor routine
 // would apply beta to a C the emulator may already have written): it returns an execution error.
 //
@@ -280,6 +285,32 @@ bool host_stream(rocblas_handle h, hipStream_t *st) {
            pm == rocblas_pointer_mode_host && a.rbGetStream(h, st) == rocblas_status_success;
 }
 
+// the emulator's type of an Ex call whose three matrices share a type the emulator covers and whose
+// compute type asks for at least that precision; -1: forward
+int ex_type(hipDataType a, hipDataType b, hipDataType c, hipblasComputeType_t ct) {
+    if (a != b || a != c) return -1;
+    if (ct == HIPBLAS_COMPUTE_64F) return a == HIP_R_64F ? GEMMUL8_R_64F : (a == HIP_C_64F ? GEMMUL8_C_64F : -1);
+    if (ct == HIPBLAS_COMPUTE_32F) return a == HIP_R_32F ? GEMMUL8_R_32F : (a == HIP_C_32F ? GEMMUL8_C_32F : -1);
+    return -1;
+}
+int ex_type(rocblas_datatype a, rocblas_datatype b, rocblas_datatype c, rocblas_datatype d, rocblas_datatype ct) {
+    if (a != b || a != c || a != d || a != ct) return -1;
+    switch (a) {
+    case rocblas_datatype_f64_r: return GEMMUL8_R_64F;
+    case rocblas_datatype_f64_c: return GEMMUL8_C_64F;
+    case rocblas_datatype_f32_r: return GEMMUL8_R_32F;
+    case rocblas_datatype_f32_c: return GEMMUL8_C_32F;
+    default: return -1;
+    }
+}
+const Mode &mode_of(int type) { return type == GEMMUL8_R_64F || type == GEMMUL8_C_64F ? cfg().d : cfg().s; }
+size_t elem_bytes(int type) {
+    return type == GEMMUL8_C_64F ? 16 : (type == GEMMUL8_R_32F ? 4 : 8);
+}
+const char *cbyte(const void *p, long long elems, int type) {
+    return static_cast<const char *>(p) + elems * (long long)elem_bytes(type);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- hipBLAS
@@ -332,6 +363,53 @@ OZ2_HIPBLAS_GEMM(hipblasSgemm, float, GEMMUL8_R_32F, s)
 OZ2_HIPBLAS_GEMM(hipblasCgemm, hipComplex, GEMMUL8_C_32F, s)
 OZ2_HIPBLAS_GEMM_SB(hipblasDgemmStridedBatched, double, GEMMUL8_R_64F, d)
 OZ2_HIPBLAS_GEMM_SB(hipblasZgemmStridedBatched, hipDoubleComplex, GEMMUL8_C_64F, d)
+OZ2_HIPBLAS_GEMM_SB(hipblasSgemmStridedBatched, float, GEMMUL8_R_32F, s)
+OZ2_HIPBLAS_GEMM_SB(hipblasCgemmStridedBatched, hipComplex, GEMMUL8_C_32F, s)
+
+hipblasStatus_t hipblasGemmEx(hipblasHandle_t handle, hipblasOperation_t transA, hipblasOperation_t transB, int m, int n,
+                              int k, const void *alpha, const void *A, hipDataType aType, int lda, const void *B,
+                              hipDataType bType, int ldb, const void *beta, void *C, hipDataType cType, int ldc,
+                              hipblasComputeType_t computeType, hipblasGemmAlgo_t algo) {
+    static auto real = next_symbol<decltype(&hipblasGemmEx)>("hipblasGemmEx");
+    const int t = ex_type(aType, bType, cType, computeType);
+    hipStream_t st = nullptr;
+    if (t >= 0 && host_stream(handle, &st)) {
+        const Outcome o = emulate("hipblasGemmEx", mode_of(t), st, (int)transA, (int)transB, m, n, k, t, alpha, A, lda,
+                                  B, ldb, beta, C, ldc);
+        if (o == Outcome::emulated) return HIPBLAS_STATUS_SUCCESS;
+        if (o == Outcome::failed) return HIPBLAS_STATUS_EXECUTION_FAILED;
+    }
+    return real ? real(handle, transA, transB, m, n, k, alpha, A, aType, lda, B, bType, ldb, beta, C, cType, ldc,
+                       computeType, algo)
+                : HIPBLAS_STATUS_NOT_SUPPORTED;
+}
+
+hipblasStatus_t hipblasGemmStridedBatchedEx(hipblasHandle_t handle, hipblasOperation_t transA,
+                                            hipblasOperation_t transB, int m, int n, int k, const void *alpha,
+                                            const void *A, hipDataType aType, int lda, hipblasStride strideA,
+                                            const void *B, hipDataType bType, int ldb, hipblasStride strideB,
+                                            const void *beta, void *C, hipDataType cType, int ldc,
+                                            hipblasStride strideC, int batchCount, hipblasComputeType_t computeType,
+                                            hipblasGemmAlgo_t algo) {
+    static auto real = next_symbol<decltype(&hipblasGemmStridedBatchedEx)>("hipblasGemmStridedBatchedEx");
+    const int t = ex_type(aType, bType, cType, computeType);
+    hipStream_t st = nullptr;
+    int b = 0;
+    if (t >= 0 && batchCount > 0 && host_stream(handle, &st))
+        for (; b < batchCount; ++b) {
+            const Outcome o = emulate("hipblasGemmStridedBatchedEx", mode_of(t), st, (int)transA, (int)transB, m, n, k,
+                                      t, alpha, cbyte(A, b * strideA, t), lda, cbyte(B, b * strideB, t), ldb, beta,
+                                      const_cast<char *>(cbyte(C, b * strideC, t)), ldc);
+            if (o == Outcome::failed) return HIPBLAS_STATUS_EXECUTION_FAILED;
+            if (o == Outcome::forward) break;
+        }
+    if (b == batchCount && batchCount > 0) return HIPBLAS_STATUS_SUCCESS;
+    if (!real) return HIPBLAS_STATUS_NOT_SUPPORTED;
+    const int tt = t >= 0 ? t : GEMMUL8_R_64F;  // (b = 0 whenever the type is not one of the emulated four)
+    return real(handle, transA, transB, m, n, k, alpha, cbyte(A, b * strideA, tt), aType, lda, strideA,
+                cbyte(B, b * strideB, tt), bType, ldb, strideB, beta, const_cast<char *>(cbyte(C, b * strideC, tt)),
+                cType, ldc, strideC, batchCount - b, computeType, algo);
+}
 }
 
 // ---------------------------------------------------------------- rocBLAS
@@ -351,9 +429,89 @@ OZ2_HIPBLAS_GEMM_SB(hipblasZgemmStridedBatched, hipDoubleComplex, GEMMUL8_C_64F,
                     : rocblas_status_not_implemented;                                                              \
     }
 
+#define OZ2_ROCBLAS_GEMM_SB(NAME, T, TYPE, MODE)                                                                   \
+    rocblas_status NAME(rocblas_handle handle, rocblas_operation transA, rocblas_operation transB, rocblas_int m, \
+                        rocblas_int n, rocblas_int k, const T *alpha, const T *A, rocblas_int lda,               \
+                        rocblas_stride strideA, const T *B, rocblas_int ldb, rocblas_stride strideB,             \
+                        const T *beta, T *C, rocblas_int ldc, rocblas_stride strideC, rocblas_int batchCount) {  \
+        static auto real = next_symbol<decltype(&NAME)>(#NAME);                                                    \
+        hipStream_t st = nullptr;                                                                                  \
+        int b = 0;                                                                                                 \
+        if (batchCount > 0 && host_stream(handle, &st))                                                           \
+            for (; b < batchCount; ++b) {                                                                          \
+                const Outcome o = emulate(#NAME, cfg().MODE, st, (int)transA, (int)transB, m, n, k, TYPE, alpha,  \
+                                          A + b * strideA, lda, B + b * strideB, ldb, beta, C + b * strideC, ldc); \
+                if (o == Outcome::failed) return rocblas_status_internal_error;                                    \
+                if (o == Outcome::forward) break;                                                                  \
+            }                                                                                                      \
+        if (b == batchCount && batchCount > 0) return rocblas_status_success;                                      \
+        return real ? real(handle, transA, transB, m, n, k, alpha, A + b * strideA, lda, strideA, B + b * strideB, \
+                           ldb, strideB, beta, C + b * strideC, ldc, strideC, batchCount - b)                      \
+                    : rocblas_status_not_implemented;                                                              \
+    }
+
+#undef rocblas_gemm_ex
+#undef rocblas_gemm_strided_batched_ex
+
 extern "C" {
 OZ2_ROCBLAS_GEMM(rocblas_dgemm, double, GEMMUL8_R_64F, d)
 OZ2_ROCBLAS_GEMM(rocblas_zgemm, rocblas_double_complex, GEMMUL8_C_64F, d)
 OZ2_ROCBLAS_GEMM(rocblas_sgemm, float, GEMMUL8_R_32F, s)
 OZ2_ROCBLAS_GEMM(rocblas_cgemm, rocblas_float_complex, GEMMUL8_C_32F, s)
+OZ2_ROCBLAS_GEMM_SB(rocblas_dgemm_strided_batched, double, GEMMUL8_R_64F, d)
+OZ2_ROCBLAS_GEMM_SB(rocblas_zgemm_strided_batched, rocblas_double_complex, GEMMUL8_C_64F, d)
+OZ2_ROCBLAS_GEMM_SB(rocblas_sgemm_strided_batched, float, GEMMUL8_R_32F, s)
+OZ2_ROCBLAS_GEMM_SB(rocblas_cgemm_strided_batched, rocblas_float_complex, GEMMUL8_C_32F, s)
+
+// D = alpha op(A) op(B) + beta C: emulated in place (d == c, ldd == ldc) only
+rocblas_status rocblas_gemm_ex(rocblas_handle handle, rocblas_operation transA, rocblas_operation transB, rocblas_int m,
+                               rocblas_int n, rocblas_int k, const void *alpha, const void *a, rocblas_datatype a_type,
+                               rocblas_int lda, const void *b, rocblas_datatype b_type, rocblas_int ldb,
+                               const void *beta, const void *c, rocblas_datatype c_type, rocblas_int ldc, void *d,
+                               rocblas_datatype d_type, rocblas_int ldd, rocblas_datatype compute_type,
+                               rocblas_gemm_algo algo, int32_t solution_index, uint32_t flags) {
+    static auto real = next_symbol<decltype(&rocblas_gemm_ex)>("rocblas_gemm_ex");
+    const int t = ex_type(a_type, b_type, c_type, d_type, compute_type);
+    hipStream_t st = nullptr;
+    if (t >= 0 && c == d && ldc == ldd && host_stream(handle, &st)) {
+        const Outcome o = emulate("rocblas_gemm_ex", mode_of(t), st, (int)transA, (int)transB, m, n, k, t, alpha, a,
+                                  lda, b, ldb, beta, d, ldd);
+        if (o == Outcome::emulated) return rocblas_status_success;
+        if (o == Outcome::failed) return rocblas_status_internal_error;
+    }
+    return real ? real(handle, transA, transB, m, n, k, alpha, a, a_type, lda, b, b_type, ldb, beta, c, c_type, ldc, d,
+                       d_type, ldd, compute_type, algo, solution_index, flags)
+                : rocblas_status_not_implemented;
+}
+
+rocblas_status rocblas_gemm_strided_batched_ex(rocblas_handle handle, rocblas_operation transA, rocblas_operation transB,
+                                               rocblas_int m, rocblas_int n, rocblas_int k, const void *alpha,
+                                               const void *a, rocblas_datatype a_type, rocblas_int lda,
+                                               rocblas_stride stride_a, const void *b, rocblas_datatype b_type,
+                                               rocblas_int ldb, rocblas_stride stride_b, const void *beta,
+                                               const void *c, rocblas_datatype c_type, rocblas_int ldc,
+                                               rocblas_stride stride_c, void *d, rocblas_datatype d_type,
+                                               rocblas_int ldd, rocblas_stride stride_d, rocblas_int batch_count,
+                                               rocblas_datatype compute_type, rocblas_gemm_algo algo,
+                                               int32_t solution_index, uint32_t flags) {
+    static auto real = next_symbol<decltype(&rocblas_gemm_strided_batched_ex)>("rocblas_gemm_strided_batched_ex");
+    const int t = ex_type(a_type, b_type, c_type, d_type, compute_type);
+    hipStream_t st = nullptr;
+    int bi = 0;
+    if (t >= 0 && c == d && ldc == ldd && stride_c == stride_d && batch_count > 0 && host_stream(handle, &st))
+        for (; bi < batch_count; ++bi) {
+            const Outcome o = emulate("rocblas_gemm_strided_batched_ex", mode_of(t), st, (int)transA, (int)transB, m, n,
+                                      k, t, alpha, cbyte(a, bi * stride_a, t), lda, cbyte(b, bi * stride_b, t), ldb,
+                                      beta, const_cast<char *>(cbyte(d, bi * stride_d, t)), ldd);
+            if (o == Outcome::failed) return rocblas_status_internal_error;
+            if (o == Outcome::forward) break;
+        }
+    if (bi == batch_count && batch_count > 0) return rocblas_status_success;
+    if (!real) return rocblas_status_not_implemented;
+    const int tt = t >= 0 ? t : GEMMUL8_R_64F;  // (bi = 0 whenever the type is not one of the emulated four)
+    return real(handle, transA, transB, m, n, k, alpha, cbyte(a, bi * stride_a, tt), a_type, lda, stride_a,
+                cbyte(b, bi * stride_b, tt), b_type, ldb, stride_b, beta, cbyte(c, bi * stride_c, tt), c_type, ldc,
+                stride_c, const_cast<char *>(cbyte(d, bi * stride_d, tt)), d_type, ldd, stride_d, batch_count - bi,
+                compute_type, algo, solution_index, flags);
+}
 }

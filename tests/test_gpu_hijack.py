@@ -177,6 +177,115 @@ print("RESULT " + json.dumps(out))
 '''
 
 
+# The Ex and strided-batched forms called directly (no framework uses them for fp64): hipblasGemmEx /
+# hipblasGemmStridedBatchedEx with the 64F compute type are emulated, the pedantic compute type is
+# forwarded; rocblas_gemm_ex in place (d == c) is emulated, out of place forwarded;
+# rocblas_dgemm_strided_batched and rocblas_zgemm_strided_batched are emulated per batch.
+CHILD_EX = r'''
+import ctypes, json, os, sys
+hj = ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)
+import torch
+sys.path.insert(0, sys.argv[2])
+import gemmul8 as G
+torch.matmul(torch.ones(4, 4, dtype=torch.float64, device="cuda"), torch.ones(4, 4, dtype=torch.float64, device="cuda"))
+hb = ctypes.CDLL("libhipblas.so.3", mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
+rb = ctypes.CDLL("librocblas.so.5", mode=os.RTLD_NOLOAD | os.RTLD_LAZY)
+st = torch.cuda.current_stream().cuda_stream
+h = ctypes.c_void_p(); assert hb.hipblasCreate(ctypes.byref(h)) == 0; hb.hipblasSetStream(h, ctypes.c_void_p(st))
+r = ctypes.c_void_p(); assert rb.rocblas_create_handle(ctypes.byref(r)) == 0; rb.rocblas_set_stream(r, ctypes.c_void_p(st))
+g = torch.Generator(device="cuda").manual_seed(9)
+I, P, L = ctypes.c_int, ctypes.c_void_p, ctypes.c_longlong
+m, n, k = 384, 320, 448
+out = {}
+def emu(A, B, dt, Cin=None, beta=0.0, ct=0):
+    C = torch.zeros((n, m), dtype=dt, device="cuda") if Cin is None else Cin.clone()
+    W = G.alloc_work(m, n, k, 14, ct)
+    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, beta, C, m, 14, True, W, ct)
+    return C
+def mats(dt, batch=None):
+    sh = lambda a, b: (a, b) if batch is None else (batch, a, b)
+    if dt.is_complex:
+        mk = lambda a, b: torch.complex(torch.randn(*sh(a, b), dtype=torch.float64, device="cuda", generator=g),
+                                        torch.randn(*sh(a, b), dtype=torch.float64, device="cuda", generator=g))
+    else:
+        mk = lambda a, b: torch.randn(*sh(a, b), dtype=dt, device="cuda", generator=g)
+    return mk(k, m), mk(n, k), mk(n, m)
+one, half = ctypes.c_double(1.0), ctypes.c_double(0.5)
+z1, zh = (ctypes.c_double * 2)(1.0, 0.0), (ctypes.c_double * 2)(0.5, 0.0)
+# hipblasGemmEx, HIP_R_64F, HIPBLAS_COMPUTE_64F (7), then _PEDANTIC (8)
+A, B, C0 = mats(torch.float64)
+for ct, key in ((7, "gemmex"), (8, "gemmex_pedantic")):
+    C = C0.clone()
+    rc = hj.hipblasGemmEx(h, 111, 111, m, n, k, ctypes.byref(one), P(A.data_ptr()), 1, m, P(B.data_ptr()), 1, k,
+                          ctypes.byref(half), P(C.data_ptr()), 1, m, ct, 160)
+    torch.cuda.synchronize()
+    Cv = C0.clone()
+    rcv = -1
+    if ct == 8:  # the vendor routine itself (for 64F it would call rocblas_gemm_ex, which is interposed too)
+        rcv = hb.hipblasGemmEx(h, 111, 111, m, n, k, ctypes.byref(one), P(A.data_ptr()), 1, m, P(B.data_ptr()), 1, k,
+                               ctypes.byref(half), P(Cv.data_ptr()), 1, m, ct, 160)
+    torch.cuda.synchronize()
+    out[key] = {"rc": rc, "bits": bool(torch.equal(C, emu(A, B, torch.float64, C0, 0.5))),
+                "vendor_rc": rcv, "vendor_bits": bool(torch.equal(C, Cv))}
+# hipblasGemmStridedBatchedEx, HIP_C_64F, 3 batches
+A, B, C0 = mats(torch.complex128, 3)
+C = C0.clone()
+rc = hj.hipblasGemmStridedBatchedEx(h, 111, 111, m, n, k, z1, P(A.data_ptr()), 5, m, L(k * m), P(B.data_ptr()), 5, k,
+                                    L(n * k), zh, P(C.data_ptr()), 5, m, L(n * m), 3, 7, 160)
+torch.cuda.synchronize()
+out["gemm_sb_ex"] = {"rc": rc, "bits": all(bool(torch.equal(C[i], emu(A[i], B[i], torch.complex128, C0[i], 0.5, 1)))
+                                       for i in range(3))}
+# rocblas_gemm_ex in place and out of place (f64_r = 152)
+A, B, C0 = mats(torch.float64)
+C = C0.clone()
+rc = hj.rocblas_gemm_ex(r, 111, 111, m, n, k, ctypes.byref(one), P(A.data_ptr()), 152, m, P(B.data_ptr()), 152, k,
+                        ctypes.byref(half), P(C.data_ptr()), 152, m, P(C.data_ptr()), 152, m, 152, 0, 0, 0)
+torch.cuda.synchronize()
+out["rocblas_gemm_ex"] = {"rc": rc, "bits": bool(torch.equal(C, emu(A, B, torch.float64, C0, 0.5)))}
+D = torch.zeros_like(C0)
+rc = hj.rocblas_gemm_ex(r, 111, 111, m, n, k, ctypes.byref(one), P(A.data_ptr()), 152, m, P(B.data_ptr()), 152, k,
+                        ctypes.byref(half), P(C0.data_ptr()), 152, m, P(D.data_ptr()), 152, m, 152, 0, 0, 0)
+torch.cuda.synchronize()
+out["rocblas_gemm_ex_out_of_place"] = {"rc": rc, "relerr": float(((D - (A.t() @ B.t()).t() - 0.5 * C0).abs().max()
+                                                               / D.abs().max()))}
+# rocblas_dgemm_strided_batched / rocblas_zgemm_strided_batched
+for name, dt, a1, ah, ct in (("rocblas_dgemm_strided_batched", torch.float64, ctypes.byref(one), ctypes.byref(half), 0),
+                             ("rocblas_zgemm_strided_batched", torch.complex128, z1, zh, 1)):
+    A, B, C0 = mats(dt, 2)
+    C = C0.clone()
+    rc = getattr(hj, name)(r, 111, 111, m, n, k, a1, P(A.data_ptr()), m, L(k * m), P(B.data_ptr()), k, L(n * k), ah,
+                           P(C.data_ptr()), m, L(n * m), 2)
+    torch.cuda.synchronize()
+    out[name] = {"rc": rc, "bits": all(bool(torch.equal(C[i], emu(A[i], B[i], dt, C0[i], 0.5, ct))) for i in range(2))}
+print("RESULT " + json.dumps(out))
+'''
+
+
+def test_ex_and_batched_forms():
+    assert os.path.exists(HIJACK), "libgemmul8_hijack.so not built"
+    env = dict(os.environ, GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14")
+    r = subprocess.run([sys.executable, "-c", CHILD_EX, HIJACK, os.path.join(ROOT, "mixed-gemmul8_amd")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1][len("RESULT "):])
+    log = r.stderr
+    assert res["gemmex"]["rc"] == 0 and res["gemmex"]["bits"], res
+    assert "[gemmul8] hipblasGemmEx m=384 n=320 k=448 -> emulated" in log, log[-2000:]
+    # the pedantic compute type goes to the vendor routine: the same status and C as calling it directly
+    # (this hipBLAS answers HIPBLAS_STATUS_NOT_SUPPORTED for it)
+    pd = res["gemmex_pedantic"]
+    assert pd["rc"] == pd["vendor_rc"] and pd["vendor_bits"], res
+    assert log.count("hipblasGemmEx m=384") == 1, log[-2000:]
+    assert res["gemm_sb_ex"]["rc"] == 0 and res["gemm_sb_ex"]["bits"], res
+    assert log.count("hipblasGemmStridedBatchedEx m=384 n=320 k=448 -> emulated") == 3, log[-2000:]
+    assert res["rocblas_gemm_ex"]["rc"] == 0 and res["rocblas_gemm_ex"]["bits"], res
+    assert log.count("rocblas_gemm_ex m=384") == 1, log[-2000:]  # out of place: forwarded
+    assert res["rocblas_gemm_ex_out_of_place"]["rc"] == 0 and res["rocblas_gemm_ex_out_of_place"]["relerr"] < 1e-13, res
+    for name in ("rocblas_dgemm_strided_batched", "rocblas_zgemm_strided_batched"):
+        assert res[name]["rc"] == 0 and res[name]["bits"], (name, res)
+        assert log.count(f"[gemmul8] {name} m=384 n=320 k=448 -> emulated") == 2, log[-2000:]
+
+
 def test_torch_matmul_is_emulated():
     assert os.path.exists(HIJACK), "libgemmul8_hijack.so not built"
     env = dict(os.environ, GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14")
