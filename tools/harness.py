@@ -1,11 +1,18 @@
 #!/usr/bin/env python3
-"""harness.py -- the reference's test drivers (GEMMul8/testing/test_double.cu, test_float.cu)
-restated over the MI355X library, with the same sweeps and the same CSV schema, so results
-line up with the published tables (GEMMul8/testing/results_in_paper/*.csv).
+"""harness.py -- the reference's test drivers (GEMMul8/testing/test_double.cu, test_float.cu,
+test_mixed_double.cu, test_mixed_float.cu, test_float_complex.cu) restated over the MI355X library,
+with the same sweeps and the same CSV schema, so results line up with the published tables
+(GEMMul8/testing/results_in_paper/*.csv).
 
     python tools/harness.py d accuracy_check flops_check [--out-dir DIR] [--sizes ...]
 
-type   d: DGEMM emulation (test_double.cu)      f: SGEMM emulation (test_float.cu)
+type   d:   DGEMM emulation (test_double.cu)             f:  SGEMM emulation (test_float.cu)
+       dfd: A f64 x B f32 -> C f64 (test_mixed_double.cu) dff: A f64 x B f32 -> C f32 (test_mixed_float.cu)
+       fC:  complex f32, COMPLEX_KARATSUBA_MULT (test_float_complex.cu)
+       TFLOPS = 2mnk / time for every type, fC included, as the reference's CSVs have it (multiply
+       by 4 for complex flops).  The sweep defaults follow each driver (moduli 2..20 and phi 0.5..4 for d / dfd; 2..15 and
+       phi 0..1.5 for f / dff / fC).  The reference's "SGEMM-TF32" / "CGEMM-TF32" rows have no
+       MI355X counterpart and are not written.
 modes  accuracy_check  oz2_results_<t>_accuracy_<device>_<date>.csv
                        "phi,function,2,...,20," rows DGEMM (k=K) / OS2-fast (k=K) / OS2-accu (k=K)
                        of max relative error (test_double.cu:70-200)
@@ -16,8 +23,9 @@ modes  accuracy_check  oz2_results_<t>_accuracy_<device>_<date>.csv
                        are this build's {scaling, int8 products, 0 (fused), CRT} in seconds
        watt_check      oz2_results_<t>_watt_<device>_<date>.csv (test_double.cu:498-745), when the
                        amdsmi Python module is importable; skipped otherwise
-Inputs: the reference generator (make_matrix.hpp:8-21, hiprand XORWOW, seed 123456, A and B from
-the same seed); errors against the double-double product (eval.hpp:265-338).
+Inputs: the reference generator (make_matrix.hpp:8-71, hiprand XORWOW, seed 123456, A and B from
+the same seed); errors against the double-double product for real types (eval.hpp:265-338), against
+the FP64 complex product for fC (|C - Cref| / |Cref| with complex abs, eval.hpp:360-379).
 """
 import argparse
 import datetime
@@ -35,6 +43,15 @@ SEED = 123456
 PHI = [0.5, 1, 2, 3, 4]
 SIZE = [1024, 2048, 4096, 8192]
 NUM_MODULI = list(range(2, 21))
+# per driver: (A, B, C) dtypes, compute type, vendor routine name, default phi list, default moduli
+F64, F32, C64 = torch.float64, torch.float32, torch.complex64
+TYPES = {
+    "d": ((F64, F64, F64), 0, "DGEMM", PHI, NUM_MODULI),
+    "f": ((F32, F32, F32), 0, "SGEMM", [0.0, 0.5, 1, 1.5], list(range(2, 16))),
+    "dfd": ((F64, F32, F64), 0, "DGEMM", PHI, NUM_MODULI),
+    "dff": ((F64, F32, F32), 0, "SGEMM", [0.0, 0.5, 1, 1.5], list(range(2, 16))),
+    "fC": ((C64, C64, C64), 3, "CGEMM", [0.0, 0.5, 1, 1.5], list(range(2, 16))),
+}
 PHASE_HDR = "conv_64f_2_8i,gpublasGemmEx,conv_32i_2_8u,inverse_scaling,"
 
 
@@ -47,7 +64,11 @@ def sync():
 
 
 def relerr(C, C1, C2):
-    """max / median of |C - (C1 + C2)| / |C1 + C2| in double-double (eval.hpp:317-338)"""
+    """max / median of |C - (C1 + C2)| / |C1 + C2| in double-double (eval.hpp:317-338); complex C
+    against the FP64 product C1 (C2 unused): |C - C1| / |C1| (eval.hpp:360-379)"""
+    if C.is_complex():
+        e = ((C.to(torch.complex128) - C1).abs() / C1.abs()).flatten()
+        return float(e.max()), float(e.median())
     return G.relerr_dd(C.to(torch.float64) if C.dtype != torch.float64 else C, C1, C2)
 
 
@@ -65,35 +86,46 @@ def timed(fn, iters):
 
 
 class Problem:
-    """column-major A (m x k), B (k x n) from the reference generator, and the dd product"""
+    """column-major A (m x k), B (k x n) from the reference generator, and the reference product"""
 
     def __init__(self, t, m, n, k, phi):
-        dt = torch.float64 if t == "d" else torch.float32
-        self.m, self.n, self.k, self.dt = m, n, k, dt
-        self.A = G.randmat(m, k, dt, phi, SEED)
-        self.B = G.randmat(k, n, dt, phi, SEED)
-        self.C = torch.empty((n, m), dtype=dt, device="cuda")
-        self.C1, self.C2 = G.dd_gemm(self.A.to(torch.float64), self.B.to(torch.float64), m, n, k)
+        (ta, tb, tc), self.ct, self.vend_name, _, _ = TYPES[t]
+        self.m, self.n, self.k = m, n, k
+        self.A = G.randmat(m, k, ta, phi, SEED)
+        self.B = G.randmat(k, n, tb, phi, SEED)
+        self.C = torch.empty((n, m), dtype=tc, device="cuda")
+        if tc.is_complex:  # FP64 complex product of the upcast operands (test_float_complex.cu:328)
+            self.C1 = torch.matmul(self.A.t().to(torch.complex128), self.B.t().to(torch.complex128)).t().contiguous()
+            self.C2 = None
+        else:
+            self.C1, self.C2 = G.dd_gemm(self.A.to(torch.float64), self.B.to(torch.float64), m, n, k)
+        # the vendor routine's operands: DGEMM on B upcast (test_mixed_double.cu:139), SGEMM on A
+        # downcast (test_mixed_float.cu:158), else the operands as they are
+        self.vA = self.A.to(tc) if tc != ta else self.A
+        self.vB = self.B.to(tc) if tc != tb else self.B
 
     def vendor(self):
         """C = A B through the vendor GEMM (torch.matmul -> hipBLAS), stored column-major"""
-        self.C.copy_(torch.matmul(self.A.t(), self.B.t()).t())
+        self.C.copy_(torch.matmul(self.vA.t(), self.vB.t()).t())
 
     def emulate(self, N, fast, work, phases=False):
         return G.gemm(G.OP_N, G.OP_N, self.m, self.n, self.k, 1.0, self.A, self.m, self.B, self.k, 0.0, self.C,
-                      self.m, N, fast, work, phase_times=phases)
+                      self.m, N, fast, work, self.ct, phase_times=phases)
+
+    def work(self, N):
+        return G.alloc_work(self.m, self.n, self.k, N, self.ct)
 
 
 def accuracy_check(t, out, args):
     name = os.path.join(out, f"oz2_results_{t}_accuracy_{device_name()}_{args.stamp}.csv")
     m = n = 1024
-    vend = "DGEMM" if t == "d" else "SGEMM"
+    vend = TYPES[t][2]
     with open(name, "w") as f:
         f.write("phi,function," + "".join(f"{N}," for N in args.moduli) + "\n")
         for phi in args.phi:
             for k in args.ksizes:
                 P = Problem(t, m, n, k, phi)
-                work = G.alloc_work(m, n, k, max(args.moduli))
+                work = P.work(max(args.moduli))
                 P.vendor()
                 sync()
                 emax, _ = relerr(P.C, P.C1, P.C2)
@@ -113,14 +145,14 @@ def accuracy_check(t, out, args):
 def flops_check(t, out, args):
     name = os.path.join(out, f"oz2_results_{t}_time_{device_name()}_{args.stamp}.csv")
     phi = 0.5
-    vend = "DGEMM" if t == "d" else "SGEMM"
+    vend = TYPES[t][2]
     with open(name, "w") as f:
         f.write("phi,m,n,k,function,relerr_max,relerr_med,TFLOPS,total_time [sec]," + PHASE_HDR + "\n")
         for s in args.sizes:
             m = n = k = s
             P = Problem(t, m, n, k, phi)
-            work = G.alloc_work(m, n, k, max(args.moduli))
-            flops = 2.0 * m * n * k
+            work = P.work(max(args.moduli))
+            flops = 2.0 * m * n * k  # fC too: the reference prints 2mnk (test_float_complex.cu:355)
             # INT8-GEMM: one int8 product of the emulator's own kernel (all-ones operands)
             L = G.layout(m, n, k, 2)
             work[L["offA"]:L["offB"] + L["planeB"] * 2].fill_(1)
@@ -196,14 +228,14 @@ def watt_check(t, out, args):
         return w, flops * reps / dt / w * 1e-9
 
     name = os.path.join(out, f"oz2_results_{t}_watt_{device_name()}_{args.stamp}.csv")
-    vend = "DGEMM" if t == "d" else "SGEMM"
+    vend = TYPES[t][2]
     with open(name, "w") as f:
         f.write("phi,m,n,k,function,relerr_max,relerr_med,watt,GFLOPS/watt,\n")
         for s in args.sizes:
             m = n = k = s
             P = Problem(t, m, n, k, 0.5)
-            work = G.alloc_work(m, n, k, max(args.moduli))
-            flops = 2.0 * m * n * k
+            work = P.work(max(args.moduli))
+            flops = 2.0 * m * n * k  # fC too: the reference prints 2mnk (test_float_complex.cu:355)
             P.vendor()
             sync()
             emax, emed = relerr(P.C, P.C1, P.C2)
@@ -222,15 +254,17 @@ def watt_check(t, out, args):
 
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
-    ap.add_argument("type", choices=["d", "f"])
+    ap.add_argument("type", choices=list(TYPES))
     ap.add_argument("modes", nargs="+", choices=["accuracy_check", "flops_check", "watt_check", "all"])
     ap.add_argument("--out-dir", default=".")
     ap.add_argument("--sizes", type=int, nargs="+", default=SIZE)
     ap.add_argument("--ksizes", type=int, nargs="+", default=SIZE)
-    ap.add_argument("--phi", type=float, nargs="+", default=PHI)
-    ap.add_argument("--moduli", type=int, nargs="+", default=NUM_MODULI)
+    ap.add_argument("--phi", type=float, nargs="+", default=None, help="default: the driver's list")
+    ap.add_argument("--moduli", type=int, nargs="+", default=None, help="default: the driver's list")
     ap.add_argument("--iters", type=int, default=100)
     args = ap.parse_args(argv)
+    args.phi = args.phi or TYPES[args.type][3]
+    args.moduli = args.moduli or TYPES[args.type][4]
     args.stamp = datetime.datetime.now().strftime("%Y-%m-%d_%H-%M-%S")
     os.makedirs(args.out_dir, exist_ok=True)
     modes = {"accuracy_check", "flops_check", "watt_check"} if "all" in args.modes else set(args.modes)
