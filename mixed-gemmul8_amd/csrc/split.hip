@@ -126,6 +126,26 @@ __device__ __forceinline__ int compute_sft(float amax, float vecnrm, float log2M
     return min(__float2int_rd(log2M - 1.0f), kk) - ilogbf(amax);
 }
 
+// Accurate mode: the reference scales the 6-bit magnitudes with the int sft0 = 5 - ilogb(amax)
+// (scaling.hpp:1909-1925) and keeps its int16 in sftA for the shift that follows.  The two differ
+// only for amax = Inf: 5 - INT_MAX sends every finite magnitude to 0, its int16 (6) does not.  That
+// case is stored as SFT0_INF, which neither finite amax (sft0 in [-1018, 1079]) nor amax = 0 can
+// produce, and its two readers map it back: sft0_scale (the magnitude encode) to the int,
+// sft0_stored (the final shift) to the int16.
+constexpr int16_t SFT0_INF = INT16_MIN;
+template <typename R> __device__ __forceinline__ int ilogb_r(R x) {
+    return std::is_same<R, double>::value ? ilogb((double)x) : ilogbf((float)x);
+}
+template <typename R> __device__ __forceinline__ int16_t sft0_of(R amax) {
+    return __builtin_isinf(amax) ? SFT0_INF : (int16_t)(5 - ilogb_r<R>(amax));
+}
+template <typename R> __device__ __forceinline__ int sft0_scale(int16_t s) {
+    return s == SFT0_INF ? 5 - ilogb_r<R>(R(INFINITY)) : (int)s;
+}
+__device__ __forceinline__ int sft0_stored(int16_t s) {
+    return s == SFT0_INF ? (int)(int16_t)(5 - ilogb((double)INFINITY)) : (int)s;
+}
+
 template <typename R, bool CPLX>
 __device__ __forceinline__ void load_elem(const R *__restrict__ X, size_t idx, R &re, R &im) {
     if constexpr (CPLX) {
@@ -222,8 +242,7 @@ __device__ __forceinline__ void stats_contig_body(const R *__restrict__ X, size_
         R mx = lane < VT / 64 ? gmax[lane] : R(0);
         mx = wave_max<R>(mx);
         if (ACCU) {
-            if (lane == 0 && v < nvec)
-                sft_out[v] = (int16_t)(5 - (std::is_same<R, double>::value ? ilogb((double)mx) : ilogbf((float)mx)));
+            if (lane == 0 && v < nvec) sft_out[v] = sft0_of<R>(mx);
         } else {
             R s2 = (lane >= 32 && lane - 32 < VT / 32) ? grp[lane - 32] : R(0);
             s2 = ref_wave_sum<R>(s2);
@@ -316,8 +335,7 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
         R mx = lane < SLOTS ? pmax[r2][lane] : R(0);
         mx = wave_max<R>(mx);
         if (ACCU) {
-            if (lane == 0 && v2 < nvec)
-                sft_out[v2] = (int16_t)(5 - (std::is_same<R, double>::value ? ilogb((double)mx) : ilogbf((float)mx)));
+            if (lane == 0 && v2 < nvec) sft_out[v2] = sft0_of<R>(mx);
             continue;
         }
         R gv = 0;
@@ -698,7 +716,7 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
     const size_t v = v0 + vl;
     const size_t kk = e0 + 16 * c;
     int s = 0;
-    if (v < nvec) s = MODE == 0 ? -(int)sft[v] : (int)sft[v];
+    if (v < nvec) s = MODE == 0 ? -(int)sft[v] : sft0_scale<R>(sft[v]);
 
     R yr[16], yi[16];
 #pragma unroll
@@ -763,7 +781,7 @@ __global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, c
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nvec) return;
     const int amax = cplx_rows ? max(bound[v], bound[v + nvec]) : bound[v];
-    const int s = (int)sft0[v] + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
+    const int s = sft0_stored(sft0[v]) + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
     sft_out[v] = (int16_t)(-s);
 }
 

@@ -717,3 +717,17 @@ def test_persistent_planes_beyond_4gib():
             assert r.returncode == 0, r.stderr[-3000:]
             outs.append(np.load(out))
         assert np.array_equal(outs[0].view(np.uint64), outs[1].view(np.uint64))
+
+
+@pytest.mark.parametrize("fast", [True, False])
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_nonfinite_inputs(fast, dtype):
+    """NaN / +-Inf in A and B: shifts, slices, residues and C equal the oracle's bit for bit (the
+    live comparison with the reference's build is tests/test_ref_parity.py::test_nonfinite_inputs_same_bits)."""
+    rng = np.random.default_rng(31)
+    A, B = randmat_np(rng, 70, 90).astype(dtype), randmat_np(rng, 90, 50).astype(dtype)
+    A[4, 10] = np.nan
+    A[9, 3] = np.inf
+    B[7, 8] = -np.inf
+    B[20, 30] = np.nan
+    check_full(A, B, 12 if dtype == np.float64 else 7, fast=fast)

@@ -104,3 +104,107 @@ def test_same_inputs_same_bits(case):
     with open(os.path.join(ROOT, "gpurun_out", "ref_compare.json"), "w") as f:
         json.dump(RESULTS, f, indent=1)
     assert same and nbad == 0, f"{nbad} elements differ from the reference"
+
+
+def _extreme(X, vec_axis, big, tiny, sub):
+    """Vectors of a column-major matrix held as a torch tensor overwritten with extreme magnitudes
+    (vec_axis 1: the rows of A, X[e, v]; 0: the columns of B, X[v, e]): vector 0 subnormal, 1 alternating big / tiny, 2 a single subnormal element, 3 zero, 4 big (its
+    sum of squares overflows), 5 negative zeros and one normal element."""
+    import torch
+    V = X if vec_axis == 1 else X.t()  # V[e, v]: element e of vector v
+    V[:, 0] *= sub
+    alt = torch.ones(V.shape[0], dtype=V.real.dtype if V.is_complex() else V.dtype, device=V.device)
+    alt[0::2] = big
+    alt[1::2] = tiny
+    V[:, 1] *= alt
+    V[:, 2] = 0
+    V[V.shape[0] // 2, 2] = sub
+    V[:, 3] = 0
+    V[:, 4] *= big
+    V[:, 5] = -0.0
+    V[1, 5] = 0.75
+    return X
+
+
+# (ta, tb, tc, m, n, k, num_moduli, fast, computeType)
+@pytest.mark.parametrize("case", [
+    ("d", "d", "d", 300, 260, 500, 14, 1, 0),
+    ("d", "d", "d", 300, 260, 500, 14, 0, 0),
+    ("d", "d", "d", 300, 260, 500, 20, 1, 0),
+    ("s", "s", "s", 200, 190, 300, 8, 1, 0),
+    ("s", "s", "s", 200, 190, 300, 8, 0, 0),
+    ("d", "s", "d", 200, 190, 300, 12, 1, 0),
+    ("z", "z", "z", 160, 150, 200, 12, 1, 1),
+    ("z", "z", "z", 160, 150, 200, 12, 0, 1),
+    ("c", "c", "c", 160, 150, 200, 7, 0, 3),    # Karatsuba (complex double only up to 7 moduli: DESIGN 10.5)
+    ("z", "z", "z", 160, 150, 200, 6, 1, 2),    # classic
+])
+def test_extreme_magnitudes_same_bits(case):
+    """Subnormal, zero, single-element and overflowing-norm rows of A and columns of B: the shifts the
+    reference derives from them (log2 of round-up sums that under- or overflow, ilogb of subnormals)
+    and everything after them give the same C bits, NaN / Inf included, as the reference's own build."""
+    import torch
+    import gemmul8 as G
+    ta, tb, tc, m, n, k, N, fast, ct = case
+    lib = _ref()
+    tdt = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}
+    dbl = {"d": True, "s": False, "z": True, "c": False}
+    A = G.randmat(m, k, tdt[ta], 0.5, 123456)  # (k, m) tensor: A[e, v] = element e of row v
+    B = G.randmat(k, n, tdt[tb], 0.5, 654321)  # (n, k) tensor: B[v, e] = element e of column v
+    ext = lambda d: (1e200, 1e-200, 1e-310) if dbl[d] else (1e25, 1e-25, 1e-40)
+    _extreme(A, 1, *ext(ta))
+    _extreme(B, 0, *ext(tb))
+    C_ref = torch.zeros((n, m), dtype=tdt[tc], device="cuda")
+    C_new = torch.zeros_like(C_ref)
+    npt = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}[tc]
+    one, zero = np.array([1], npt), np.array([0], npt)
+    wref = torch.zeros(lib.ref_work_size(m, n, k, N, ct) + 16 * A.numel() + (1 << 20), dtype=torch.uint8,
+                       device="cuda")
+    rc = lib.ref_gemm(CODES[ta], CODES[tb], CODES[tc], 0, 0, m, n, k, one.ctypes.data, A.data_ptr(), m,
+                      B.data_ptr(), k, zero.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
+    assert rc == 0
+    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C_new, m, N, bool(fast), G.alloc_work(m, n, k, N, ct), ct)
+    torch.cuda.synchronize()
+    a = C_ref.view(torch.uint8).cpu().numpy()
+    b = C_new.view(torch.uint8).cpu().numpy()
+    nbad = int((a != b).sum())
+    assert nbad == 0, f"{nbad} bytes differ from the reference"
+    # the inputs did reach the interesting regimes: the normal part of C is finite and nonzero
+    assert torch.isfinite(C_new[6:, 6:]).all() and (C_new[6:, 6:] != 0).any()
+
+
+@pytest.mark.parametrize("case", [
+    ("d", 14, 1, 0), ("d", 14, 0, 0), ("s", 8, 1, 0), ("z", 12, 1, 1), ("c", 7, 0, 3),
+])
+def test_nonfinite_inputs_same_bits(case):
+    """A NaN in one row of A, +Inf in one column of B and -Inf in another: C matches the reference's
+    build byte for byte, whatever the non-finite shifts make of the affected rows and columns."""
+    import torch
+    import gemmul8 as G
+    t, N, fast, ct = case
+    m, n, k = 130, 120, 140
+    lib = _ref()
+    tdt = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}[t]
+    A = G.randmat(m, k, tdt, 0.5, 123456)
+    B = G.randmat(k, n, tdt, 0.5, 654321)
+    A[7, 5] = float("nan")       # row 5 of A, element 7
+    B[9, 3] = float("inf")       # column 9 of B, element 3
+    B[11, 100] = -float("inf")   # column 11 of B, element 100
+    C_ref = torch.zeros((n, m), dtype=tdt, device="cuda")
+    C_new = torch.zeros_like(C_ref)
+    npt = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}[t]
+    one, zero = np.array([1], npt), np.array([0], npt)
+    wref = torch.zeros(lib.ref_work_size(m, n, k, N, ct) + 16 * A.numel() + (1 << 20), dtype=torch.uint8,
+                       device="cuda")
+    rc = lib.ref_gemm(CODES[t], CODES[t], CODES[t], 0, 0, m, n, k, one.ctypes.data, A.data_ptr(), m, B.data_ptr(), k,
+                      zero.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
+    assert rc == 0
+    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C_new, m, N, bool(fast), G.alloc_work(m, n, k, N, ct), ct)
+    torch.cuda.synchronize()
+    bad = (C_ref.view(torch.uint8) != C_new.view(torch.uint8))
+    nbad = int(bad.sum())
+    if nbad:
+        nan_ref, nan_new = torch.isnan(C_ref), torch.isnan(C_new)
+        print("differing bytes", nbad, "NaN ref", int(nan_ref.sum()), "NaN new", int(nan_new.sum()),
+              "same NaN pattern", bool(torch.equal(nan_ref, nan_new)))
+    assert nbad == 0, f"{nbad} bytes differ from the reference"
