@@ -173,38 +173,39 @@ def test_extreme_magnitudes_same_bits(case):
     assert torch.isfinite(C_new[6:, 6:]).all() and (C_new[6:, 6:] != 0).any()
 
 
+# (ta, tb, tc, num_moduli, fast, computeType, opA, opB)
 @pytest.mark.parametrize("case", [
-    ("d", 14, 1, 0), ("d", 14, 0, 0), ("s", 8, 1, 0), ("z", 12, 1, 1), ("c", 7, 0, 3),
+    ("d", "d", "d", 14, 1, 0, 0, 0), ("d", "d", "d", 14, 0, 0, 0, 0), ("s", "s", "s", 8, 1, 0, 0, 0),
+    ("z", "z", "z", 12, 1, 1, 0, 0), ("c", "c", "c", 7, 0, 3, 0, 0),
+    ("d", "d", "d", 14, 0, 0, 1, 1), ("d", "s", "d", 12, 0, 0, 0, 0), ("s", "d", "s", 8, 0, 0, 1, 0),
+    ("z", "z", "z", 12, 0, 1, 0, 0), ("z", "z", "z", 6, 0, 2, 0, 2), ("c", "c", "c", 7, 1, 3, 1, 0),
 ])
 def test_nonfinite_inputs_same_bits(case):
     """A NaN in one row of A, +Inf in one column of B and -Inf in another: C matches the reference's
     build byte for byte, whatever the non-finite shifts make of the affected rows and columns."""
     import torch
     import gemmul8 as G
-    t, N, fast, ct = case
+    ta, tb, tc, N, fast, ct, opA, opB = case
     m, n, k = 130, 120, 140
     lib = _ref()
-    tdt = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}[t]
-    A = G.randmat(m, k, tdt, 0.5, 123456)
-    B = G.randmat(k, n, tdt, 0.5, 654321)
-    A[7, 5] = float("nan")       # row 5 of A, element 7
-    B[9, 3] = float("inf")       # column 9 of B, element 3
-    B[11, 100] = -float("inf")   # column 11 of B, element 100
-    C_ref = torch.zeros((n, m), dtype=tdt, device="cuda")
+    tdt = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}
+    # stored column-major: op N A is m x k (tensor (k, m)), op T A is k x m (tensor (m, k)); likewise B
+    A = G.randmat(k, m, tdt[ta], 0.5, 123456) if opA else G.randmat(m, k, tdt[ta], 0.5, 123456)
+    B = G.randmat(n, k, tdt[tb], 0.5, 654321) if opB else G.randmat(k, n, tdt[tb], 0.5, 654321)
+    A[7, 5] = float("nan")
+    B[9, 3] = float("inf")
+    B[11, 100] = -float("inf")
+    lda, ldb = (k if opA else m), (n if opB else k)
+    C_ref = torch.zeros((n, m), dtype=tdt[tc], device="cuda")
     C_new = torch.zeros_like(C_ref)
-    npt = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}[t]
+    npt = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}[tc]
     one, zero = np.array([1], npt), np.array([0], npt)
     wref = torch.zeros(lib.ref_work_size(m, n, k, N, ct) + 16 * A.numel() + (1 << 20), dtype=torch.uint8,
                        device="cuda")
-    rc = lib.ref_gemm(CODES[t], CODES[t], CODES[t], 0, 0, m, n, k, one.ctypes.data, A.data_ptr(), m, B.data_ptr(), k,
-                      zero.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
+    rc = lib.ref_gemm(CODES[ta], CODES[tb], CODES[tc], opA, opB, m, n, k, one.ctypes.data, A.data_ptr(), lda,
+                      B.data_ptr(), ldb, zero.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
     assert rc == 0
-    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C_new, m, N, bool(fast), G.alloc_work(m, n, k, N, ct), ct)
+    G.gemm(opA, opB, m, n, k, 1.0, A, lda, B, ldb, 0.0, C_new, m, N, bool(fast), G.alloc_work(m, n, k, N, ct), ct)
     torch.cuda.synchronize()
-    bad = (C_ref.view(torch.uint8) != C_new.view(torch.uint8))
-    nbad = int(bad.sum())
-    if nbad:
-        nan_ref, nan_new = torch.isnan(C_ref), torch.isnan(C_new)
-        print("differing bytes", nbad, "NaN ref", int(nan_ref.sum()), "NaN new", int(nan_new.sum()),
-              "same NaN pattern", bool(torch.equal(nan_ref, nan_new)))
+    nbad = int((C_ref.view(torch.uint8) != C_new.view(torch.uint8)).sum())
     assert nbad == 0, f"{nbad} bytes differ from the reference"
