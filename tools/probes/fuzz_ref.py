@@ -2,7 +2,8 @@
 """Randomised LIVE parity sweep: this library against the reference's own build (oracle/_ref,
 tests/test_ref_parity.py) on identical device inputs, C compared byte for byte.  Random shapes,
 type combinations, moduli counts, modes, ops, complex compute types and alpha/beta, minus the
-input classes DESIGN.md section 10 lists as reference defects.  python fuzz_ref.py [cases] [seed]
+input classes DESIGN.md section 10 lists as reference defects.
+python fuzz_ref.py [cases] [seed] [m_n_lo:m_n_hi k_lo:k_hi]
 Writes gpurun_out/fuzz_ref.json."""
 import json
 import os
@@ -21,6 +22,7 @@ COMBOS = [("d", "d", "d"), ("s", "s", "s"), ("d", "s", "d"), ("s", "d", "d"), ("
           ("z", "z", "z"), ("c", "c", "c"), ("c", "z", "z"), ("z", "c", "z"), ("z", "c", "c"), ("c", "z", "c")]
 TDT = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}
 NPT = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}
+MN, K = (1, 600), (1, 1400)
 
 
 def defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab):
@@ -54,13 +56,17 @@ def defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab):
 def main():
     cases = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     rng = np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 1)
+    global MN, K
+    if len(sys.argv) > 4:  # size ranges: m, n in [a, b), k in [c, d)
+        MN, K = tuple(map(int, sys.argv[3].split(":"))), tuple(map(int, sys.argv[4].split(":")))
     lib = _ref()
     t0 = time.time()
-    ran, fails, skipped, unchanged = 0, [], {}, 0
+    ran, fails, skipped, unchanged = 0, [], {}, []
     while ran < cases:
         ta, tb, tc = COMBOS[rng.integers(len(COMBOS))]
         cplx = ta in "cz"
-        m, n, k = int(rng.integers(1, 600)), int(rng.integers(1, 600)), int(rng.integers(1, 1400))
+        m, n = int(rng.integers(MN[0], MN[1])), int(rng.integers(MN[0], MN[1]))
+        k = int(rng.integers(K[0], K[1]))
         N = int(rng.integers(2, 21))
         fast = int(rng.integers(2))
         ct = int(rng.integers(1, 4)) if cplx else 0
@@ -86,20 +92,21 @@ def main():
                complex(ab[1]) if cplx else ab[1], C_new, m, N, bool(fast), G.alloc_work(m, n, k, N, ct), ct)
         torch.cuda.synchronize()
         nbad = int((C_ref.view(torch.uint8) != C_new.view(torch.uint8)).sum())
-        unchanged += bool(torch.equal(C_new.view(torch.uint8), C0.view(torch.uint8)))  # a call that wrote nothing
+        desc = dict(types=ta + tb + tc, m=m, n=n, k=k, N=N, fast=fast, ct=ct, op=[opA, opB], alpha=ab[0],
+                    beta=ab[1], phi=phi, seed=seed, rc=rc, bytes_differ=nbad)
+        if torch.equal(C_new.view(torch.uint8), C0.view(torch.uint8)):  # a call that changed nothing
+            unchanged.append(desc)
         ran += 1
         if rc != 0 or nbad:
-            desc = dict(types=ta + tb + tc, m=m, n=n, k=k, N=N, fast=fast, ct=ct, op=[opA, opB], alpha=ab[0],
-                        beta=ab[1], phi=phi, seed=seed, rc=rc, bytes_differ=nbad)
             fails.append(desc)
             print("FAIL", desc, flush=True)
         if ran % 50 == 0:
             print(f"{ran} cases, {len(fails)} failures, {time.time() - t0:.0f} s", flush=True)
     out = dict(cases=ran, failures=fails, outputs_left_unchanged=unchanged, skipped_defect_classes=skipped, seconds=time.time() - t0)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "fuzz_ref.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", os.environ.get("FUZZ_OUT", "fuzz_ref.json")), "w") as f:
         json.dump(out, f, indent=1)
-    print(f"{ran} cases, {len(fails)} failures, {unchanged} outputs unchanged, skipped {skipped}, "
+    print(f"{ran} cases, {len(fails)} failures, {len(unchanged)} outputs unchanged, skipped {skipped}, "
           f"{time.time() - t0:.0f} s", flush=True)
     sys.exit(1 if fails else 0)
 
