@@ -130,27 +130,45 @@ template <> struct BlasEpi<1> {
         return epi_f(v, c, (float)a.ar, (float)a.br);
     }
 };
-// Complex outputs.  With real alpha and beta (ai = bi = 0) each component takes the real-scalar form,
-// so a non-finite Im(C) cannot reach Re(C) through a 0 * Inf term; for finite values it gives the bits
-// of the full complex form (whose zero-imaginary terms only add signed zeros), and for alpha = beta = 1
-// it is the reference's component-wise CAdd (inverse_scaling.hpp:370-392).
+// Complex outputs: the reference's kernels operation for operation (inverse_scaling.hpp:268-948), with
+// hip_complex.h's hipCmul / hipCfma as clang contracts them in its build (pinned on the reference's own
+// full-precision outputs, tools/probes/epi_dump2.py; hipCmul's imaginary part fuses p.x*q.y in f64 and
+// p.y*q.x in f32):
+//   alpha = 1, beta = 0: v (_10);  alpha = beta = 1: C + v per component (CAdd, _11);
+//   beta = 1: hipCfma(alpha, v, C) (_a1);  otherwise hipCfma(beta, C, hipCmul(alpha, v)) (_ab).
+// Two departures, both BLAS semantics: beta = 0 does not read C (the reference's _ab does),
+// and alpha = 1 with another beta is hipCfma(beta, C, v) (the reference's _1b computes beta*AB + C, 10.3).
+template <typename R, typename R2> struct CplxEpi {
+    static __device__ __forceinline__ R fma_(R a, R b, R c) {
+        if constexpr (sizeof(R) == 8) return __builtin_fma(a, b, c);
+        else return __builtin_fmaf(a, b, c);
+    }
+    static __device__ __forceinline__ R2 mk(R x, R y) { return R2{x, y}; }
+    static __device__ __forceinline__ R2 cmul(R pr, R pi, R qr, R qi) {  // hipCmul(p, q)
+        // the imaginary part's fused product differs between the reference's f64 and f32 builds
+        if constexpr (sizeof(R) == 8) return mk(fma_(pr, qr, -(pi * qi)), fma_(pr, qi, pi * qr));
+        else return mk(fma_(pr, qr, -(pi * qi)), fma_(pi, qr, pr * qi));
+    }
+    static __device__ __forceinline__ R2 cfma(R pr, R pi, R qr, R qi, R rr, R ri) {  // hipCfma(p, q, r)
+        R re = fma_(pr, qr, rr), im = fma_(qr, pi, ri);
+        return mk(fma_(-pi, qi, re), fma_(pr, qi, im));
+    }
+    static __device__ __forceinline__ R2 f(R2 v, R2 c, R ar, R ai, R br, R bi) {
+        const bool a1 = ar == R(1) && ai == R(0);
+        if (br == R(0) && bi == R(0)) return a1 ? v : cmul(ar, ai, v.x, v.y);
+        if (br == R(1) && bi == R(0)) return a1 ? mk(c.x + v.x, c.y + v.y) : cfma(ar, ai, v.x, v.y, c.x, c.y);
+        const R2 x = a1 ? v : cmul(ar, ai, v.x, v.y);
+        return cfma(br, bi, c.x, c.y, x.x, x.y);
+    }
+};
 template <> struct BlasEpi<2> {
     static __device__ __forceinline__ double2 f(double2 v, double2 c, const CrtArgs &a) {
-        if (a.ai == 0.0 && a.bi == 0.0)
-            return make_double2(__builtin_fma(a.br, c.x, a.ar * v.x), __builtin_fma(a.br, c.y, a.ar * v.y));
-        const double tr = __builtin_fma(a.ar, v.x, -a.ai * v.y), ti = __builtin_fma(a.ar, v.y, a.ai * v.x);
-        return make_double2(__builtin_fma(a.br, c.x, __builtin_fma(-a.bi, c.y, tr)),
-                            __builtin_fma(a.br, c.y, __builtin_fma(a.bi, c.x, ti)));
+        return CplxEpi<double, double2>::f(v, c, a.ar, a.ai, a.br, a.bi);
     }
 };
 template <> struct BlasEpi<3> {
     static __device__ __forceinline__ float2 f(float2 v, float2 c, const CrtArgs &a) {
-        const float arf = (float)a.ar, aif = (float)a.ai, brf = (float)a.br, bif = (float)a.bi;
-        if (aif == 0.0f && bif == 0.0f)
-            return make_float2(__builtin_fmaf(brf, c.x, arf * v.x), __builtin_fmaf(brf, c.y, arf * v.y));
-        const float tr = __builtin_fmaf(arf, v.x, -aif * v.y), ti = __builtin_fmaf(arf, v.y, aif * v.x);
-        return make_float2(__builtin_fmaf(brf, c.x, __builtin_fmaf(-bif, c.y, tr)),
-                           __builtin_fmaf(brf, c.y, __builtin_fmaf(bif, c.x, ti)));
+        return CplxEpi<float, float2>::f(v, c, (float)a.ar, (float)a.ai, (float)a.br, (float)a.bi);
     }
 };
 

@@ -569,6 +569,34 @@ static float epi_f(float v, float c, float al, float be, int quirks) {
     return fmaf(be, c, al * v);
 }
 
+/* Complex epilogue: the reference's kernels operation for operation, with hip_complex.h's
+ * hipCmul(p, q) = (fma(p.x, q.x, -(p.y*q.y)), fma(p.x, q.y, p.y*q.x)) in f64 (f32: the imaginary part
+ * fma(p.y, q.x, p.x*q.y)) and hipCfma(p, q, r) =
+ * (fma(-p.y, q.y, fma(p.x, q.x, r.x)), fma(p.x, q.y, fma(q.x, p.y, r.y))) as clang contracts them
+ * (inverse_scaling.hpp:268-948): alpha = 1, beta = 0: v; alpha = beta = 1: C + v (CAdd); beta = 1:
+ * hipCfma(alpha, v, C); otherwise hipCfma(beta, C, hipCmul(alpha, v)).  BLAS departures as the GPU
+ * build: beta = 0 does not read C, alpha = 1 with another beta is hipCfma(beta, C, v). */
+#define OZ2O_CEPI(NAME, R, FMA, IM_F64)                                                                      \
+    static void NAME(R vr, R vi, R cr, R ci, R ar, R ai, R br, R bi, R *outr, R *outi) {                    \
+        int a1 = ar == (R)1 && ai == (R)0;                                                                    \
+        R xr = vr, xi = vi;                                                                                   \
+        if (!a1) {                                                                                            \
+            xr = FMA(ar, vr, -(ai * vi));                                                                     \
+            xi = IM_F64 ? FMA(ar, vi, ai * vr) : FMA(ai, vr, ar * vi);                                        \
+        }                                                                                                     \
+        if (br == (R)0 && bi == (R)0) { *outr = xr; *outi = xi; return; }                                   \
+        if (br == (R)1 && bi == (R)0) {                                                                       \
+            if (a1) { *outr = cr + vr; *outi = ci + vi; return; }                                             \
+            R re = FMA(ar, vr, cr), im = FMA(vr, ai, ci);                                                     \
+            *outr = FMA(-ai, vi, re); *outi = FMA(ar, vi, im); return;                                        \
+        }                                                                                                     \
+        R re = FMA(br, cr, xr), im = FMA(cr, bi, xi);                                                         \
+        *outr = FMA(-bi, ci, re); *outi = FMA(br, ci, im);                                                    \
+    }
+OZ2O_CEPI(cepi_d, double, fma, 1)
+OZ2O_CEPI(cepi_f, float, fmaf, 0)
+#undef OZ2O_CEPI
+
 /* tc: output type; m, n: logical C size; R planes of size mr*n (mr = m or 2m) */
 int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint8_t *R, const int16_t *sftA,
              const int16_t *sftB, const void *alpha, const void *beta, void *C, size_t ldc, int quirks) {
@@ -597,34 +625,13 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
                     double *Cz = (double *)C;
                     int zb = be[0] == 0.0 && be[1] == 0.0;
                     double cr = zb ? 0.0 : Cz[2 * o], ci = zb ? 0.0 : Cz[2 * o + 1];
-                    if (al[0] == 1.0 && al[1] == 0.0 && be[0] == 0.0 && be[1] == 0.0) {
-                        Cz[2 * o] = vr; Cz[2 * o + 1] = vi;
-                    } else if (al[1] == 0.0 && be[1] == 0.0) {
-                        /* real alpha, beta: per component (alpha = beta = 1 is the reference's CAdd,
-                         * inverse_scaling.hpp:370-392); no 0*Inf from Im(C) into Re(C) */
-                        Cz[2 * o] = fma(be[0], cr, al[0] * vr);
-                        Cz[2 * o + 1] = fma(be[0], ci, al[0] * vi);
-                    } else { /* alpha*v + beta*c, products fused as the GPU build does */
-                        double tr = fma(al[0], vr, -al[1] * vi), ti = fma(al[0], vi, al[1] * vr);
-                        Cz[2 * o] = fma(be[0], cr, fma(-be[1], ci, tr));
-                        Cz[2 * o + 1] = fma(be[0], ci, fma(be[1], cr, ti));
-                    }
+                    cepi_d(vr, vi, cr, ci, al[0], al[1], be[0], be[1], &Cz[2 * o], &Cz[2 * o + 1]);
                 } else {
                     const float *al = (const float *)alpha, *be = (const float *)beta;
                     float *Cc = (float *)C;
-                    float fr = (float)vr, fi = (float)vi;
                     int zb = be[0] == 0.0f && be[1] == 0.0f;
                     float cr = zb ? 0.0f : Cc[2 * o], ci = zb ? 0.0f : Cc[2 * o + 1];
-                    if (al[0] == 1.0f && al[1] == 0.0f && be[0] == 0.0f && be[1] == 0.0f) {
-                        Cc[2 * o] = fr; Cc[2 * o + 1] = fi;
-                    } else if (al[1] == 0.0f && be[1] == 0.0f) {
-                        Cc[2 * o] = fmaf(be[0], cr, al[0] * fr);
-                        Cc[2 * o + 1] = fmaf(be[0], ci, al[0] * fi);
-                    } else {
-                        float tr = fmaf(al[0], fr, -al[1] * fi), ti = fmaf(al[0], fi, al[1] * fr);
-                        Cc[2 * o] = fmaf(be[0], cr, fmaf(-be[1], ci, tr));
-                        Cc[2 * o + 1] = fmaf(be[0], ci, fmaf(be[1], cr, ti));
-                    }
+                    cepi_f((float)vr, (float)vi, cr, ci, al[0], al[1], be[0], be[1], &Cc[2 * o], &Cc[2 * o + 1]);
                 }
             }
         }

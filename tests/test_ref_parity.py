@@ -209,3 +209,43 @@ def test_nonfinite_inputs_same_bits(case):
     torch.cuda.synchronize()
     nbad = int((C_ref.view(torch.uint8) != C_new.view(torch.uint8)).sum())
     assert nbad == 0, f"{nbad} bytes differ from the reference"
+
+
+# (type, num_moduli, computeType, alpha, beta, non-finite Im(C))
+@pytest.mark.parametrize("case", [
+    ("z", 6, 1, 1.5 - 0.5j, 0.0, False), ("c", 6, 1, 1.5 - 0.5j, 0.0, False),
+    ("z", 6, 1, 1.5 - 0.5j, 0.25 + 0.75j, False), ("c", 6, 1, 1.5 - 0.5j, 0.25 + 0.75j, False),
+    ("z", 6, 1, 1.0 + 1.0j, 1.0, False), ("c", 6, 1, 1.0 + 1.0j, 1.0, False),
+    ("c", 6, 1, 2.5, 1.0, False), ("z", 14, 1, 2.5, -0.5j, False), ("c", 8, 1, 2.5, 0.5, False),
+    ("z", 14, 1, 1.5 - 0.5j, 0.0, False), ("z", 14, 1, 1.5 - 0.5j, 0.25 + 0.75j, False),
+    ("z", 19, 1, 0.3 + 1.7j, -1.25 + 0.5j, False), ("c", 12, 1, 0.3 + 1.7j, -1.25 + 0.5j, False),
+    ("z", 6, 1, 1.0, 1.0, True), ("c", 6, 1, 2.0, 0.5, True), ("z", 6, 1, 2.5, 1.0, True),
+    ("z", 6, 1, 1.5 - 0.5j, 0.25 + 0.75j, True), ("c", 7, 3, 1.0, 0.0, True), ("z", 6, 2, 1.0, 0.0, True),
+])
+def test_complex_alpha_beta_same_bits(case):
+    """Complex and general alpha / beta through the reference's epilogue kernels (_a1, _ab, CAdd),
+    finite and with Inf / NaN in Im(C): the same bytes as the reference's build.  (alpha = 1 with
+    another beta (_1b) and beta = 0 reading C are the reference's non-BLAS variants)"""
+    import torch
+    import gemmul8 as G
+    t, N, ct, al, be, nonfinite = case
+    m, n, k = 150, 130, 256
+    lib = _ref()
+    tdt = {"z": torch.complex128, "c": torch.complex64}[t]
+    npt = {"z": np.complex128, "c": np.complex64}[t]
+    A = G.randmat(m, k, tdt, 0.5, 123456)
+    B = G.randmat(k, n, tdt, 0.5, 654321)
+    C0 = G.randmat(m, n, tdt, 0.5, 777)
+    if nonfinite:
+        C0[4, 3] = complex(0.5, float("inf"))
+        C0[9, 11] = complex(-0.25, float("nan"))
+    C_ref, C_new = C0.clone(), C0.clone()
+    alpha, beta = np.array([al], npt), np.array([be], npt)
+    wref = torch.zeros(lib.ref_work_size(m, n, k, N, ct) + (1 << 22), dtype=torch.uint8, device="cuda")
+    rc = lib.ref_gemm(CODES[t], CODES[t], CODES[t], 0, 0, m, n, k, alpha.ctypes.data, A.data_ptr(), m, B.data_ptr(), k,
+                      beta.ctypes.data, C_ref.data_ptr(), m, N, 1, ct, wref.data_ptr(), None)
+    assert rc == 0
+    G.gemm(0, 0, m, n, k, complex(al), A, m, B, k, complex(be), C_new, m, N, True, G.alloc_work(m, n, k, N, ct), ct)
+    torch.cuda.synchronize()
+    nbad = int((C_ref.view(torch.uint8) != C_new.view(torch.uint8)).sum())
+    assert nbad == 0, f"{nbad} bytes differ from the reference"
