@@ -24,7 +24,8 @@ TDT = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch
 NPT = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}
 MN, K = (1, 600), (1, 1400)
 EXTREME = os.environ.get("FUZZ_EXTREME") == "1"
-AB = os.environ.get("FUZZ_AB", "basic")  # "general": complex and general (alpha, beta) too  # half the cases with extreme / non-finite inputs
+AB = os.environ.get("FUZZ_AB", "basic")
+LD = os.environ.get("FUZZ_LD") == "1"  # padded leading dimensions (not with FUZZ_EXTREME)  # "general": complex and general (alpha, beta) too  # half the cases with extreme / non-finite inputs
 
 
 def defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab):
@@ -91,9 +92,22 @@ def main():
             skipped[why] = skipped.get(why, 0) + 1
             continue
         seed = int(rng.integers(1 << 30))
-        A = G.randmat(k, m, TDT[ta], phi, seed) if opA else G.randmat(m, k, TDT[ta], phi, seed)
-        B = G.randmat(n, k, TDT[tb], phi, seed + 1) if opB else G.randmat(k, n, TDT[tb], phi, seed + 1)
-        special = EXTREME and rng.random() < 0.5
+        def pad_ld(base):  # FUZZ_LD: leading dimensions beyond the minimum, a fifth of them multiples of 1024
+            if not LD:
+                return base
+            if rng.random() < 0.2:
+                return max(1024, (base + 1023) // 1024 * 1024)
+            return base + int(rng.integers(0, 41))
+        lda, ldb, ldc = pad_ld(k if opA else m), pad_ld(n if opB else k), pad_ld(m)
+        if LD and ldb % 1024 == 0 and opB:
+            skipped["10.10"] = skipped.get("10.10", 0) + 1
+            continue
+        if LD and cplx and lda % 1024 == 0 and not opA:
+            skipped["10.17"] = skipped.get("10.17", 0) + 1
+            continue
+        A = G.randmat(lda, m if opA else k, TDT[ta], phi, seed)
+        B = G.randmat(ldb, k if opB else n, TDT[tb], phi, seed + 1)
+        special = EXTREME and not LD and rng.random() < 0.5
         inj = []
         if special and ab[0] != 1 and ab[1] == 0:  # the reference's _ab reads C at beta = 0: zero signs
             skipped["10.16"] = skipped.get("10.16", 0) + 1
@@ -108,8 +122,7 @@ def main():
                         rng.choice([np.nan, np.inf, -np.inf]))
                     X[i, j] = val
                     inj.append(["A" if X is A else "B", i, j, str(val)])
-        C0 = G.randmat(m, n, TDT[tc], 0.5, seed + 2)
-        lda, ldb = (k if opA else m), (n if opB else k)
+        C0 = G.randmat(ldc, n, TDT[tc], 0.5, seed + 2)
         C_ref, C_new = C0.clone(), C0.clone()
         alpha, beta = np.array([ab[0]], NPT[tc]), np.array([ab[1]], NPT[tc])
         if not cplx and (np.iscomplexobj(np.array(ab[0])) or np.iscomplexobj(np.array(ab[1]))):
@@ -117,9 +130,9 @@ def main():
         wref = torch.zeros(lib.ref_work_size(m, n, k, N, ct) + 16 * max(A.numel(), B.numel()) + (1 << 20),
                            dtype=torch.uint8, device="cuda")
         rc = lib.ref_gemm(CODES[ta], CODES[tb], CODES[tc], opA, opB, m, n, k, alpha.ctypes.data, A.data_ptr(), lda,
-                          B.data_ptr(), ldb, beta.ctypes.data, C_ref.data_ptr(), m, N, fast, ct, wref.data_ptr(), None)
+                          B.data_ptr(), ldb, beta.ctypes.data, C_ref.data_ptr(), ldc, N, fast, ct, wref.data_ptr(), None)
         G.gemm(opA, opB, m, n, k, complex(ab[0]) if cplx else ab[0], A, lda, B, ldb,
-               complex(ab[1]) if cplx else ab[1], C_new, m, N, bool(fast), G.alloc_work(m, n, k, N, ct), ct)
+               complex(ab[1]) if cplx else ab[1], C_new, ldc, N, bool(fast), G.alloc_work(m, n, k, N, ct), ct)
         torch.cuda.synchronize()
         nbad = int((C_ref.view(torch.uint8) != C_new.view(torch.uint8)).sum())
         nonfinite_only = False
@@ -140,7 +153,7 @@ def main():
             if nonfinite_only:
                 nonfinite_vec.append(int(nbad))
                 nbad = 0
-        desc = dict(special=bool(special), inj=inj, types=ta + tb + tc, m=m, n=n, k=k, N=N, fast=fast, ct=ct, op=[opA, opB], alpha=str(ab[0]),
+        desc = dict(special=bool(special), inj=inj, ld=[lda, ldb, ldc], types=ta + tb + tc, m=m, n=n, k=k, N=N, fast=fast, ct=ct, op=[opA, opB], alpha=str(ab[0]),
                     beta=str(ab[1]), phi=phi, seed=seed, rc=rc, bytes_differ=nbad)
         if torch.equal(C_new.view(torch.uint8), C0.view(torch.uint8)):  # a call that changed nothing
             unchanged.append(desc)
