@@ -146,15 +146,22 @@ __device__ __forceinline__ int sft0_stored(int16_t s) {
     return s == SFT0_INF ? (int)(int16_t)(5 - ilogb((double)INFINITY)) : (int)s;
 }
 
-template <typename R, bool CPLX>
+// NT: non-temporal loads for operands too large to stay in the Infinity Cache between the shift pass and the
+// encode (they saved 6.5 % of the split at 8192^3 and cost 5-10 % below 4096^3, where the encode's re-read
+// still hits the cache: tools/probes/nt_probe.py); the launchers pick it by operand size (use_nt).
+template <typename R, bool CPLX, bool NT = false>
 __device__ __forceinline__ void load_elem(const R *__restrict__ X, size_t idx, R &re, R &im) {
     if constexpr (CPLX) {
-        using V2 = typename std::conditional<std::is_same<R, double>::value, double2, float2>::type;
-        V2 z = reinterpret_cast<const V2 *>(X)[idx];
+        typedef R R2v __attribute__((ext_vector_type(2)));
+        const R2v *p = reinterpret_cast<const R2v *>(X) + idx;
+        R2v z;
+        if constexpr (NT) z = __builtin_nontemporal_load(p);
+        else z = *p;
         re = z.x;
         im = z.y;
     } else {
-        re = X[idx];
+        if constexpr (NT) re = __builtin_nontemporal_load(X + idx);
+        else re = X[idx];
         im = 0;
     }
 }
@@ -206,7 +213,7 @@ __device__ __forceinline__ void accum(R re, R im, R &amax, R &sum) {
 // ------------------------------------------------------------------
 // vector v by the VT threads t = 0..VT-1 of a block (or of one half of a 2 VT block: every thread of
 // the block must call it, it holds a barrier); v >= nvec computes nothing and stores nothing
-template <typename R, bool CPLX, int VT, bool ACCU>
+template <typename R, bool CPLX, int VT, bool ACCU, bool NT = false>
 __device__ __forceinline__ void stats_contig_body(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
                                                   float log2M, int16_t *__restrict__ sft_out, size_t v, int t,
                                                   R (&grp)[32], R (&gmax)[8]) {
@@ -221,13 +228,13 @@ __device__ __forceinline__ void stats_contig_body(const R *__restrict__ X, size_
     for (; e + (U - 1) * VT < len; e += U * VT) {
         R re[U], im[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) load_elem<R, CPLX>(x, e + u * VT, re[u], im[u]);
+        for (int u = 0; u < U; ++u) load_elem<R, CPLX, NT>(x, e + u * VT, re[u], im[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) accum<R, CPLX, !ACCU>(re[u], im[u], amax, sum);
     }
     for (; e < len; e += VT) {
         R re, im;
-        load_elem<R, CPLX>(x, e, re, im);
+        load_elem<R, CPLX, NT>(x, e, re, im);
         accum<R, CPLX, !ACCU>(re, im, amax, sum);
     }
     amax = wave_max<R>(amax);
@@ -251,12 +258,12 @@ __device__ __forceinline__ void stats_contig_body(const R *__restrict__ X, size_
         }
     }
 }
-template <typename R, bool CPLX, int VT, bool ACCU>
+template <typename R, bool CPLX, int VT, bool ACCU, bool NT>
 __global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
                                                          float log2M, int16_t *__restrict__ sft_out) {
     __shared__ R grp[32];
     __shared__ R gmax[8];
-    stats_contig_body<R, CPLX, VT, ACCU>(X, ld, len, nvec, log2M, sft_out, blockIdx.x, threadIdx.x, grp, gmax);
+    stats_contig_body<R, CPLX, VT, ACCU, NT>(X, ld, len, nvec, log2M, sft_out, blockIdx.x, threadIdx.x, grp, gmax);
 }
 
 // ------------------------------------------------------------------
@@ -272,7 +279,7 @@ template <typename R, int VT, int ROWS> struct StridedShared {
     R part[ROWS][VT + 1];
     R pmax[ROWS][256 / ROWS + 1];
 };
-template <typename R, bool CPLX, int VT, bool ACCU, int ROWS>
+template <typename R, bool CPLX, int VT, bool ACCU, int ROWS, bool NT = false>
 __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
                                                    float log2M, int16_t *__restrict__ sft_out, unsigned bx,
                                                    StridedShared<R, VT, ROWS> &sh) {
@@ -297,7 +304,7 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int c = 0; c < NA; ++c) load_elem<R, CPLX>(X, (b + u * VT + slot + SLOTS * c) * ld + v, re[u][c], im[u][c]);
+                for (int c = 0; c < NA; ++c) load_elem<R, CPLX, NT>(X, (b + u * VT + slot + SLOTS * c) * ld + v, re[u][c], im[u][c]);
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -306,7 +313,7 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
         for (; b + VT <= len; b += VT) {
             R re[NA], im[NA];
 #pragma unroll
-            for (int c = 0; c < NA; ++c) load_elem<R, CPLX>(X, (b + slot + SLOTS * c) * ld + v, re[c], im[c]);
+            for (int c = 0; c < NA; ++c) load_elem<R, CPLX, NT>(X, (b + slot + SLOTS * c) * ld + v, re[c], im[c]);
 #pragma unroll
             for (int c = 0; c < NA; ++c) accum<R, CPLX, !ACCU>(re[c], im[c], amax, acc[c]);
         }
@@ -316,7 +323,7 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
                 const size_t e = b + slot + SLOTS * c;
                 if (e < len) {
                     R re, im;
-                    load_elem<R, CPLX>(X, e * ld + v, re, im);
+                    load_elem<R, CPLX, NT>(X, e * ld + v, re, im);
                     accum<R, CPLX, !ACCU>(re, im, amax, acc[c]);
                 }
             }
@@ -351,17 +358,17 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
         if (lane == 0 && v2 < nvec) sft_out[v2] = (int16_t)(-compute_sft(mx, nrm, log2M));
     }
 }
-template <typename R, bool CPLX, int VT, bool ACCU, int ROWS>
+template <typename R, bool CPLX, int VT, bool ACCU, int ROWS, bool NT>
 __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
                                                            float log2M, int16_t *__restrict__ sft_out) {
     __shared__ StridedShared<R, VT, ROWS> sh;
-    stats_strided_body<R, CPLX, VT, ACCU, ROWS>(X, ld, len, nvec, log2M, sft_out, blockIdx.x, sh);
+    stats_strided_body<R, CPLX, VT, ACCU, ROWS, NT>(X, ld, len, nvec, log2M, sft_out, blockIdx.x, sh);
 }
 
 // Both operands' fast-mode shifts in one launch (small problems, one stream; real f64, A rows strided,
 // B columns contiguous, VT = 128): blocks [0, ga) sweep ROWS rows of A each, the others two columns of
 // B each (one per 128-thread half, the contiguous pass's own block shape).
-template <int ROWS>
+template <int ROWS, bool NT>
 __global__ __launch_bounds__(256) void stats_pair_kernel(const double *__restrict__ A, size_t lda, size_t m,
                                                         const double *__restrict__ B, size_t ldb, size_t n, size_t len,
                                                         float log2M, int16_t *__restrict__ sftA,
@@ -370,11 +377,11 @@ __global__ __launch_bounds__(256) void stats_pair_kernel(const double *__restric
     __shared__ double grp[2][32];
     __shared__ double gmax[2][8];
     if (blockIdx.x < ga) {
-        stats_strided_body<double, false, 128, false, ROWS>(A, lda, len, m, log2M, sftA, blockIdx.x, sh);
+        stats_strided_body<double, false, 128, false, ROWS, NT>(A, lda, len, m, log2M, sftA, blockIdx.x, sh);
     } else {
         const int half = threadIdx.x >> 7;
         const size_t v = 2 * (size_t)(blockIdx.x - ga) + half;
-        stats_contig_body<double, false, 128, false>(B, ldb, len, n, log2M, sftB, v, threadIdx.x & 127, grp[half],
+        stats_contig_body<double, false, 128, false, NT>(B, ldb, len, n, log2M, sftB, v, threadIdx.x & 127, grp[half],
                                                      gmax[half]);
     }
 }
@@ -654,7 +661,7 @@ __device__ __forceinline__ void encode_vec16(const R (&yr)[16], const R (&yi)[16
 
 template <typename R, bool CPLX> using EncTile = R[CPLX ? 32 : 64][64 + 1][CPLX ? 2 : 1];
 
-template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
+template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE, bool NTL = false>
 __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
                                             const int16_t *__restrict__ sft, int8_t *__restrict__ out, size_t plane,
                                             size_t ksteps, size_t kblk, size_t vmax, int flags, const ModParams &MP,
@@ -688,7 +695,7 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
             int vl, el;
             if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
             const size_t v = v0 + vl, e = e0 + el;
-            load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
+            load_elem<R, CPLX, NTL>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
         }
     } else {
 #pragma unroll
@@ -699,7 +706,7 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
             const size_t v = v0 + vl, e = e0 + el;
             lre[i] = 0;
             lim[i] = 0;
-            if (v < nvec && e < len) load_elem<R, CPLX>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
+            if (v < nvec && e < len) load_elem<R, CPLX, NTL>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], lim[i]);
         }
     }
 #pragma unroll
@@ -735,7 +742,7 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
     encode_vec16<R, CPLX, IS_A, MODE>(yr, yi, v, kk, nvec, len, out, plane, ksteps, kblk, vmax, flags, MP, G);
 }
 
-template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE>
+template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE, bool NTL>
 __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__restrict__ X, size_t ld, size_t nvec,
                                                                    size_t len, const int16_t *__restrict__ sft,
                                                                    int8_t *__restrict__ out, size_t plane,
@@ -743,7 +750,7 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                                                                    int flags, ModParams MP, ModGroups G) {
     __shared__ EncTile<R, CPLX> tile;
     if (MP.zero_queue && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
-    encode_body<R, CPLX, CONTIG, IS_A, MODE>(X, ld, nvec, len, sft, out, plane, ksteps, kblk, vmax, flags, MP, G,
+    encode_body<R, CPLX, CONTIG, IS_A, MODE, NTL>(X, ld, nvec, len, sft, out, plane, ksteps, kblk, vmax, flags, MP, G,
                                              blockIdx.x, blockIdx.y, tile);
 }
 
@@ -758,19 +765,19 @@ struct EncOperand {
     int flags;
     unsigned gx, gy;
 };
-template <typename R, bool CPLX, bool CONTIG_A, bool CONTIG_B>
+template <typename R, bool CPLX, bool CONTIG_A, bool CONTIG_B, bool NTL>
 __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_pair_kernel(EncOperand a, EncOperand b, size_t ksteps,
                                                                         size_t kblk, ModParams MP, ModGroups G) {
     __shared__ EncTile<R, CPLX> tile;
     const unsigned na = a.gx * a.gy;
     if (MP.zero_queue && blockIdx.x == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
     if (blockIdx.x < na) {
-        encode_body<R, CPLX, CONTIG_A, true, 0>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.sft, a.out, a.plane,
+        encode_body<R, CPLX, CONTIG_A, true, 0, NTL>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.sft, a.out, a.plane,
                                                 ksteps, kblk, a.vmax, a.flags, MP, G, blockIdx.x % a.gx, blockIdx.x / a.gx,
                                                 tile);
     } else {
         const unsigned t = blockIdx.x - na;
-        encode_body<R, CPLX, CONTIG_B, false, 0>(static_cast<const R *>(b.X), b.ld, b.nvec, b.len, b.sft, b.out, b.plane,
+        encode_body<R, CPLX, CONTIG_B, false, 0, NTL>(static_cast<const R *>(b.X), b.ld, b.nvec, b.len, b.sft, b.out, b.plane,
                                                  ksteps, kblk, b.vmax, b.flags, MP, G, t % b.gx, t / b.gx, tile);
     }
 }
@@ -811,20 +818,27 @@ static int stats_rows(size_t nvec) {
     return forced ? forced : nvec >= 4096 ? 16 : nvec >= 2048 ? 8 : 4;
 }
 
+// non-temporal operand loads from this many operand bytes (see load_elem)
+constexpr size_t NT_OPERAND_BYTES = size_t(1) << 27;
+
 template <typename R, bool CPLX>
 static void launch_stats(const void *X, size_t ld, bool contig, size_t len, size_t nvec, int VT, bool accurate,
                          float log2M, int16_t *out, hipStream_t st) {
     const R *x = static_cast<const R *>(X);
+    const bool nt = nvec * len * sizeof(R) * (CPLX ? 2 : 1) >= NT_OPERAND_BYTES;
     if (contig) {
-#define OZ2_SC(vt, ac) launch(stats_contig_kernel<R, CPLX, vt, ac>, dim3((unsigned)nvec), dim3(vt), st, x, ld, len, nvec, log2M, out)
+#define OZ2_SC(vt, ac) do { if (nt) launch(stats_contig_kernel<R, CPLX, vt, ac, true>, dim3((unsigned)nvec), dim3(vt), st, x, ld, len, nvec, log2M, out); \
+                            else launch(stats_contig_kernel<R, CPLX, vt, ac, false>, dim3((unsigned)nvec), dim3(vt), st, x, ld, len, nvec, log2M, out); } while (0)
         if (VT == 512) { if (accurate) OZ2_SC(512, true); else OZ2_SC(512, false); }
         else { if (accurate) OZ2_SC(128, true); else OZ2_SC(128, false); }
 #undef OZ2_SC
     } else {
         const int rows = stats_rows(nvec);
         const unsigned g = (unsigned)((nvec + rows - 1) / rows);
-#define OZ2_SS(vt, ac, rw) launch(stats_strided_kernel<R, CPLX, vt, ac, rw>, dim3(g), dim3(256), st, x, ld, len, nvec, log2M, out)
-#define OZ2_SSR(vt, ac) do { if (rows == 16) OZ2_SS(vt, ac, 16); else if (rows == 8) OZ2_SS(vt, ac, 8); else OZ2_SS(vt, ac, 4); } while (0)
+#define OZ2_SS(vt, ac, rw, n) launch(stats_strided_kernel<R, CPLX, vt, ac, rw, n>, dim3(g), dim3(256), st, x, ld, len, nvec, log2M, out)
+        // (operands of NT size always take 16-row blocks: stats_rows gives 16 from 4096 vectors)
+#define OZ2_SSR(vt, ac) do { if (rows == 16) { if (nt) OZ2_SS(vt, ac, 16, true); else OZ2_SS(vt, ac, 16, false); } \
+                             else if (rows == 8) OZ2_SS(vt, ac, 8, false); else OZ2_SS(vt, ac, 4, false); } while (0)
         if (VT == 512) { if (accurate) OZ2_SSR(512, true); else OZ2_SSR(512, false); }
         else { if (accurate) OZ2_SSR(128, true); else OZ2_SSR(128, false); }
 #undef OZ2_SSR
@@ -849,7 +863,9 @@ static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, si
     const dim3 grid = kf ? dim3((unsigned)(L.kblk / KT), (unsigned)(vpad_grid / 64))
                          : dim3((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
     const ModGroups G = make_groups(MP, L.N);  // grouping by the call's N (magnitude bound), not the sub-range
-#define OZ2_EN(cg, md) launch(encode_kernel<R, CPLX, cg, IS_A, md>, grid, dim3(NT), st, x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G)
+    const bool nt = nvec * len * sizeof(R) * (CPLX ? 2 : 1) >= NT_OPERAND_BYTES;
+#define OZ2_EN(cg, md) do { if (nt) launch(encode_kernel<R, CPLX, cg, IS_A, md, true>, grid, dim3(NT), st, x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G); \
+                            else launch(encode_kernel<R, CPLX, cg, IS_A, md, false>, grid, dim3(NT), st, x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G); } while (0)
     if (contig) { if (mode == 0) OZ2_EN(true, 0); else OZ2_EN(true, 1); }
     else { if (mode == 0) OZ2_EN(false, 0); else OZ2_EN(false, 1); }
 #undef OZ2_EN
@@ -894,10 +910,11 @@ bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, si
     const int rows = stats_rows(m);
     const unsigned ga = (unsigned)((m + rows - 1) / rows), gb = (unsigned)((n + 1) / 2);
     const double *a = static_cast<const double *>(dA.ptr), *b = static_cast<const double *>(dB.ptr);
-#define OZ2_SP(r) launch(stats_pair_kernel<r>, dim3(ga + gb), dim3(256), st, a, dA.ld, m, b, dB.ld, n, len, log2M, sftA, sftB, ga)
-    if (rows == 16) OZ2_SP(16);
-    else if (rows == 8) OZ2_SP(8);
-    else OZ2_SP(4);
+    const bool nt = (m + n) * len * sizeof(double) >= 2 * NT_OPERAND_BYTES;
+#define OZ2_SP(r, t) launch(stats_pair_kernel<r, t>, dim3(ga + gb), dim3(256), st, a, dA.ld, m, b, dB.ld, n, len, log2M, sftA, sftB, ga)
+    if (rows == 16) { if (nt) OZ2_SP(16, true); else OZ2_SP(16, false); }
+    else if (rows == 8) OZ2_SP(8, false);
+    else OZ2_SP(4, false);
 #undef OZ2_SP
     return true;
 }
@@ -906,8 +923,12 @@ template <typename R, bool CPLX, bool CA, bool CB>
 static void launch_encode_pair(const EncOperand &a, const EncOperand &b, const Layout &L, const ModParams &MP,
                                hipStream_t st) {
     const ModGroups G = make_groups(MP, L.N);
-    launch(encode_pair_kernel<R, CPLX, CA, CB>, dim3(a.gx * a.gy + b.gx * b.gy), dim3(CPLX ? 128 : 256), st, a, b,
-           L.ksteps, L.kblk, MP, G);
+    const dim3 grid(a.gx * a.gy + b.gx * b.gy), block(CPLX ? 128 : 256);
+    // non-temporal loads only for the real f64 form, the one large calls take (the others fork per operand)
+    if (!CPLX && sizeof(R) == 8 && (a.nvec + b.nvec) * a.len * sizeof(R) >= 2 * NT_OPERAND_BYTES)
+        launch(encode_pair_kernel<R, CPLX, CA, CB, !CPLX && sizeof(R) == 8>, grid, block, st, a, b, L.ksteps, L.kblk, MP, G);
+    else
+        launch(encode_pair_kernel<R, CPLX, CA, CB, false>, grid, block, st, a, b, L.ksteps, L.kblk, MP, G);
 }
 template <typename R, bool CPLX>
 static void launch_encode_pair_ops(bool ca, bool cb, const EncOperand &a, const EncOperand &b, const Layout &L,
