@@ -65,6 +65,9 @@ __device__ __forceinline__ double crt_value_const(const uint8_t (&r)[N], std::in
     }
 }
 
+#ifndef OZ2_CRT_NT
+#define OZ2_CRT_NT 0  // probe builds: 1 = non-temporal residue loads, 2 = non-temporal C stores, 3 = both
+#endif
 // residues of rows [off, off+8) of every plane; the fast path is one 8-byte load per plane
 template <unsigned N>
 __device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fast, int nr, uint64_t (&w)[N]) {
@@ -73,7 +76,8 @@ __device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fas
         const uint8_t *q = a.R + off;
 #pragma unroll
         for (unsigned i = 0; i < N; ++i) {
-            w[i] = *reinterpret_cast<const uint64_t *>(q);
+            if (OZ2_CRT_NT & 1) w[i] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(q));
+            else w[i] = *reinterpret_cast<const uint64_t *>(q);
             q += a.planeR;
             asm volatile("" : "+v"(q));
         }
@@ -295,7 +299,12 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
 #pragma unroll
                     for (int q = 0; q < EPV; ++q) v[q] = BlasEpi<OT>::f(v[q], c[q], a);
                 }
-                *reinterpret_cast<int4 *>(Cc + idx) = *reinterpret_cast<const int4 *>(v);
+                if (OZ2_CRT_NT & 2) {
+                    typedef int i4v __attribute__((ext_vector_type(4)));
+                    __builtin_nontemporal_store(*reinterpret_cast<const i4v *>(v), reinterpret_cast<i4v *>(Cc + idx));
+                } else {
+                    *reinterpret_cast<int4 *>(Cc + idx) = *reinterpret_cast<const int4 *>(v);
+                }
             } else {
 #pragma unroll
                 for (int q = 0; q < EPV; ++q) {

@@ -1,9 +1,9 @@
 """Split-phase time at 8192^3 (N = 14, fast) with the default build or the non-temporal-load probe build
-(tools/probes/_nt, OZ2_NT_LOADS=1).  python nt_probe.py default|nt [reps]"""
+(tools/probes/_<name>/gemmul8, e.g. a CRT build with -DOZ2_CRT_NT).  python nt_probe.py default|<name> [reps] [size]"""
 import hashlib, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 which = sys.argv[1]
-sys.path.insert(0, os.path.join(ROOT, "tools/probes/_nt") if which == "nt" else os.path.join(ROOT, "mixed-gemmul8_amd"))
+sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd") if which == "default" else os.path.join(ROOT, "tools/probes", "_" + which))
 import torch
 import gemmul8 as G
 print(which, G.LIB_PATH, flush=True)
