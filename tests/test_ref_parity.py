@@ -7,6 +7,7 @@ Also records both implementations' wall time per call into gpurun_out/ref_compar
 import ctypes
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -249,3 +250,22 @@ def test_complex_alpha_beta_same_bits(case):
     torch.cuda.synchronize()
     nbad = int((C_ref.view(torch.uint8) != C_new.view(torch.uint8)).sum())
     assert nbad == 0, f"{nbad} bytes differ from the reference"
+
+
+@pytest.mark.parametrize("mode", [
+    dict(seed=101, extreme=False, ab_mode="general", ld=False),
+    dict(seed=102, extreme=False, ab_mode="general", ld=True),
+    dict(seed=103, extreme=True, ab_mode="general", ld=False),
+])
+def test_randomized_live_parity(mode):
+    """tools/probes/fuzz_ref.py as a test: 300 random calls (the 12 type combinations, N = 2..20, both modes,
+    ops N/T/C, the three complex compute types, general and complex alpha / beta; padded leading dimensions;
+    extreme and non-finite inputs) through both builds, C compared byte for byte.  Skipped: the input classes
+    of DESIGN.md section 10; with non-finite inputs, differences confined to the rows / columns that hold them."""
+    _ref()
+    sys.path.insert(0, os.path.join(ROOT, "tools", "probes"))
+    import fuzz_ref
+    out = fuzz_ref.sweep(300, mode["seed"], extreme=mode["extreme"], ab_mode=mode["ab_mode"], ld=mode["ld"],
+                         verbose=False)
+    assert out["cases"] == 300
+    assert not out["failures"], out["failures"][:3]

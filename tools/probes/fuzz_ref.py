@@ -61,12 +61,14 @@ def defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab):
     return None
 
 
-def main():
-    cases = int(sys.argv[1]) if len(sys.argv) > 1 else 200
-    rng = np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 1)
-    global MN, K
-    if len(sys.argv) > 4:  # size ranges: m, n in [a, b), k in [c, d)
-        MN, K = tuple(map(int, sys.argv[3].split(":"))), tuple(map(int, sys.argv[4].split(":")))
+def sweep(cases, seed, mn=None, kr=None, extreme=None, ab_mode=None, ld=None, verbose=True):
+    """run `cases` random calls through both libraries; returns the summary dict (failures first)"""
+    global MN, K, EXTREME, AB, LD
+    MN, K = mn or MN, kr or K
+    EXTREME = EXTREME if extreme is None else extreme
+    AB = AB if ab_mode is None else ab_mode
+    LD = LD if ld is None else ld
+    rng = np.random.default_rng(seed)
     lib = _ref()
     t0 = time.time()
     ran, fails, skipped, unchanged, nonfinite_vec = 0, [], {}, [], []
@@ -160,10 +162,24 @@ def main():
         ran += 1
         if rc != 0 or nbad:
             fails.append(desc)
-            print("FAIL", desc, flush=True)
-        if ran % 50 == 0:
+            if verbose:
+                print("FAIL", desc, flush=True)
+        if verbose and ran % 50 == 0:
             print(f"{ran} cases, {len(fails)} failures, {time.time() - t0:.0f} s", flush=True)
-    out = dict(cases=ran, failures=fails, differ_only_in_nonfinite_vectors=len(nonfinite_vec), outputs_left_unchanged=unchanged, skipped_defect_classes=skipped, seconds=time.time() - t0)
+    return dict(cases=ran, failures=fails, differ_only_in_nonfinite_vectors=len(nonfinite_vec),
+                outputs_left_unchanged=unchanged, skipped_defect_classes=skipped, seconds=time.time() - t0)
+
+
+def main():
+    cases = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    mn = kr = None
+    if len(sys.argv) > 4:  # size ranges: m, n in [a, b), k in [c, d)
+        mn, kr = tuple(map(int, sys.argv[3].split(":"))), tuple(map(int, sys.argv[4].split(":")))
+    t0 = time.time()
+    out = sweep(cases, seed, mn, kr)
+    ran, fails, skipped = out["cases"], out["failures"], out["skipped_defect_classes"]
+    unchanged, nonfinite_vec = out["outputs_left_unchanged"], [0] * out["differ_only_in_nonfinite_vectors"]
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", os.environ.get("FUZZ_OUT", "fuzz_ref.json")), "w") as f:
         json.dump(out, f, indent=1)
