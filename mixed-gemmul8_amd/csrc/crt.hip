@@ -125,32 +125,34 @@ template <> struct OutElem<1> { using T = float; };
 template <> struct OutElem<2> { using T = double2; };
 template <> struct OutElem<3> { using T = float2; };
 
+// f<NUMM1>: the complex forms depend on the reference kernel's moduli level (below)
 template <int OT> struct BlasEpi;
 template <> struct BlasEpi<0> {
+    template <bool NUMM1>
     static __device__ __forceinline__ double f(double v, double c, const CrtArgs &a) { return epi_d(v, c, a.ar, a.br); }
 };
 template <> struct BlasEpi<1> {
+    template <bool NUMM1>
     static __device__ __forceinline__ float f(float v, float c, const CrtArgs &a) {
         return epi_f(v, c, (float)a.ar, (float)a.br);
     }
 };
 // Complex outputs: the reference's kernels operation for operation (inverse_scaling.hpp:268-948), with
 // hip_complex.h's hipCmul / hipCfma as clang contracts them in its build (pinned on the reference's own
-// full-precision outputs, tools/probes/epi_dump2.py; hipCmul's imaginary part fuses p.x*q.y in f64 and
-// p.y*q.x in f32):
+// full-precision outputs, tools/probes/epi_dump2.py, and pinned by tests/golden/ref_golden_epilogue.npz):
 //   alpha = 1, beta = 0: v (_10);  alpha = beta = 1: C + v per component (CAdd, _11);
 //   beta = 1: hipCfma(alpha, v, C) (_a1);  otherwise hipCfma(beta, C, hipCmul(alpha, v)) (_ab).
 // Two departures, both BLAS semantics: beta = 0 does not read C (the reference's _ab does),
 // and alpha = 1 with another beta is hipCfma(beta, C, v) (the reference's _1b computes beta*AB + C, 10.3).
-template <typename R, typename R2> struct CplxEpi {
+template <typename R, typename R2, bool IM_PXQY> struct CplxEpi {
     static __device__ __forceinline__ R fma_(R a, R b, R c) {
         if constexpr (sizeof(R) == 8) return __builtin_fma(a, b, c);
         else return __builtin_fmaf(a, b, c);
     }
     static __device__ __forceinline__ R2 mk(R x, R y) { return R2{x, y}; }
     static __device__ __forceinline__ R2 cmul(R pr, R pi, R qr, R qi) {  // hipCmul(p, q)
-        // the imaginary part's fused product differs between the reference's f64 and f32 builds
-        if constexpr (sizeof(R) == 8) return mk(fma_(pr, qr, -(pi * qi)), fma_(pr, qi, pi * qr));
+        // which product of the imaginary part clang fused differs between the reference's kernels
+        if constexpr (IM_PXQY) return mk(fma_(pr, qr, -(pi * qi)), fma_(pr, qi, pi * qr));
         else return mk(fma_(pr, qr, -(pi * qi)), fma_(pi, qr, pr * qi));
     }
     static __device__ __forceinline__ R2 cfma(R pr, R pi, R qr, R qi, R rr, R ri) {  // hipCfma(p, q, r)
@@ -165,14 +167,18 @@ template <typename R, typename R2> struct CplxEpi {
         return cfma(br, bi, c.x, c.y, x.x, x.y);
     }
 };
+// hipCmul's imaginary part: p.x*q.y fused in the two-level (numM = 2) complex-double kernels
+// (inverse_scaling_2_*_bigmatrix), p.y*q.x in the one-level ones and in every complex-float kernel
 template <> struct BlasEpi<2> {
+    template <bool NUMM1>
     static __device__ __forceinline__ double2 f(double2 v, double2 c, const CrtArgs &a) {
-        return CplxEpi<double, double2>::f(v, c, a.ar, a.ai, a.br, a.bi);
+        return CplxEpi<double, double2, !NUMM1>::f(v, c, a.ar, a.ai, a.br, a.bi);
     }
 };
 template <> struct BlasEpi<3> {
+    template <bool NUMM1>
     static __device__ __forceinline__ float2 f(float2 v, float2 c, const CrtArgs &a) {
-        return CplxEpi<float, float2>::f(v, c, (float)a.ar, (float)a.ai, (float)a.br, (float)a.bi);
+        return CplxEpi<float, float2, false>::f(v, c, (float)a.ar, (float)a.ai, (float)a.br, (float)a.bi);
     }
 };
 
@@ -297,7 +303,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
                         *reinterpret_cast<int4 *>(c) = *reinterpret_cast<const int4 *>(Cc + idx);
                     }
 #pragma unroll
-                    for (int q = 0; q < EPV; ++q) v[q] = BlasEpi<OT>::f(v[q], c[q], a);
+                    for (int q = 0; q < EPV; ++q) v[q] = BlasEpi<OT>::template f<NUMM1>(v[q], c[q], a);
                 }
                 if (OZ2_CRT_NT & 2) {
                     typedef int i4v __attribute__((ext_vector_type(4)));
@@ -310,7 +316,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
                 for (int q = 0; q < EPV; ++q) {
                     if (wrow0 + idx + q < a.m) {
                         E x = v[q];
-                        if (!plain_ab) x = BlasEpi<OT>::f(x, zero_beta ? E{} : Cc[idx + q], a);
+                        if (!plain_ab) x = BlasEpi<OT>::template f<NUMM1>(x, zero_beta ? E{} : Cc[idx + q], a);
                         Cc[idx + q] = x;
                     }
                 }

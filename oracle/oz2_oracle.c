@@ -570,14 +570,14 @@ static float epi_f(float v, float c, float al, float be, int quirks) {
 }
 
 /* Complex epilogue: the reference's kernels operation for operation, with hip_complex.h's
- * hipCmul(p, q) = (fma(p.x, q.x, -(p.y*q.y)), fma(p.x, q.y, p.y*q.x)) in f64 (f32: the imaginary part
- * fma(p.y, q.x, p.x*q.y)) and hipCfma(p, q, r) =
+ * hipCmul(p, q) = (fma(p.x, q.x, -(p.y*q.y)), fma(p.y, q.x, p.x*q.y)), the imaginary part
+ * fma(p.x, q.y, p.y*q.x) in the two-level complex-double kernels, and hipCfma(p, q, r) =
  * (fma(-p.y, q.y, fma(p.x, q.x, r.x)), fma(p.x, q.y, fma(q.x, p.y, r.y))) as clang contracts them
  * (inverse_scaling.hpp:268-948): alpha = 1, beta = 0: v; alpha = beta = 1: C + v (CAdd); beta = 1:
  * hipCfma(alpha, v, C); otherwise hipCfma(beta, C, hipCmul(alpha, v)).  BLAS departures as the GPU
  * build: beta = 0 does not read C, alpha = 1 with another beta is hipCfma(beta, C, v). */
-#define OZ2O_CEPI(NAME, R, FMA, IM_F64)                                                                      \
-    static void NAME(R vr, R vi, R cr, R ci, R ar, R ai, R br, R bi, R *outr, R *outi) {                    \
+#define OZ2O_CEPI(NAME, R, FMA)                                                                              \
+    static void NAME(R vr, R vi, R cr, R ci, R ar, R ai, R br, R bi, R *outr, R *outi, int IM_F64) {        \
         int a1 = ar == (R)1 && ai == (R)0;                                                                    \
         R xr = vr, xi = vi;                                                                                   \
         if (!a1) {                                                                                            \
@@ -593,8 +593,8 @@ static float epi_f(float v, float c, float al, float be, int quirks) {
         R re = FMA(br, cr, xr), im = FMA(cr, bi, xi);                                                         \
         *outr = FMA(-bi, ci, re); *outi = FMA(br, ci, im);                                                    \
     }
-OZ2O_CEPI(cepi_d, double, fma, 1)
-OZ2O_CEPI(cepi_f, float, fmaf, 0)
+OZ2O_CEPI(cepi_d, double, fma)
+OZ2O_CEPI(cepi_f, float, fmaf)
 #undef OZ2O_CEPI
 
 /* tc: output type; m, n: logical C size; R planes of size mr*n (mr = m or 2m) */
@@ -625,13 +625,13 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
                     double *Cz = (double *)C;
                     int zb = be[0] == 0.0 && be[1] == 0.0;
                     double cr = zb ? 0.0 : Cz[2 * o], ci = zb ? 0.0 : Cz[2 * o + 1];
-                    cepi_d(vr, vi, cr, ci, al[0], al[1], be[0], be[1], &Cz[2 * o], &Cz[2 * o + 1]);
+                    cepi_d(vr, vi, cr, ci, al[0], al[1], be[0], be[1], &Cz[2 * o], &Cz[2 * o + 1], !numM1);
                 } else {
                     const float *al = (const float *)alpha, *be = (const float *)beta;
                     float *Cc = (float *)C;
                     int zb = be[0] == 0.0f && be[1] == 0.0f;
                     float cr = zb ? 0.0f : Cc[2 * o], ci = zb ? 0.0f : Cc[2 * o + 1];
-                    cepi_f((float)vr, (float)vi, cr, ci, al[0], al[1], be[0], be[1], &Cc[2 * o], &Cc[2 * o + 1]);
+                    cepi_f((float)vr, (float)vi, cr, ci, al[0], al[1], be[0], be[1], &Cc[2 * o], &Cc[2 * o + 1], 0);
                 }
             }
         }

@@ -84,7 +84,8 @@ def sweep(cases, seed, mn=None, kr=None, extreme=None, ab_mode=None, ld=None, ve
         if AB == "general":  # every BLAS-consistent reference kernel (10.3: _1b and _2_a1 are not)
             pool = [(1.0, 0.0), (1.0, 1.0), (2.5, 0.0), (2.5, 0.5), (2.5, 1.0)]
             if cplx:
-                pool += [(1.5 - 0.5j, 0.0), (1.5 - 0.5j, 0.25 + 0.75j), (1.0 + 1.0j, 1.0), (2.5, -0.5j)]
+                pool += [(1.5 - 0.5j, 0.0), (1.5 - 0.5j, 0.25 + 0.75j), (1.0 + 1.0j, 1.0), (2.5, -0.5j),
+                         (0.3 + 1.7j, -1.25 + 0.5j), (0.3 + 1.7j, 0.0), (-0.7 + 0.9j, 1.0)]  # inexact ai * x
             ab = pool[rng.integers(len(pool))]
         else:
             ab = [(1.0, 0.0), (1.0, 1.0), (2.5, 0.0)][rng.integers(3)]
