@@ -11,7 +11,8 @@ LIB = os.path.join(ROOT, "mixed-gemmul8_amd", "gemmul8", "libgemmul8_amd.so")
 
 
 def _declared_c_functions():
-    txt = open(os.path.join(ROOT, "include", "gemmul8_c.h")).read()
+    with open(os.path.join(ROOT, "include", "gemmul8_c.h")) as f:
+        txt = f.read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(gemmul8_[a-z0-9_]+)\s*\(", txt)))
 
@@ -35,7 +36,8 @@ def test_c_abi_exports_every_declared_function():
 
 
 def test_cpp_symbols_match_reference():
-    ref = open(os.path.join(ROOT, "tests", "golden", "ref_symbols.txt")).read().split()
+    with open(os.path.join(ROOT, "tests", "golden", "ref_symbols.txt")) as f:
+        ref = f.read().split()
     exp = _exported()
     missing = [s for s in ref if s not in exp]
     assert not missing, missing

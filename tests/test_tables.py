@@ -26,7 +26,8 @@ def test_generated_header_is_current(tmp_path):
     out = tmp_path / "t.inc"
     gt.main.__globals__["sys"].argv = ["gen_tables.py", str(out)]
     gt.main()
-    cur = open(os.path.join(ROOT, "mixed-gemmul8_amd", "csrc", "oz2_tables.inc")).read()
+    with open(os.path.join(ROOT, "mixed-gemmul8_amd", "csrc", "oz2_tables.inc")) as f:
+        cur = f.read()
     assert out.read_text() == cur, "oz2_tables.inc is stale: run python3 tools/gen_tables.py"
 
 
