@@ -1,41 +1,53 @@
 #!/usr/bin/env python3
 """bench.py -- emulated DGEMM throughput of the MI355X Ozaki-II emulator (BASELINE.json metric).
 
-Workload (BASELINE.json configs[1], "cfg2"): DGEMM emulation, m = n = k = 8192,
-num_moduli = 14, fast mode, NN, alpha = 1, beta = 0, inputs from the reference
-driver's generator (hiprand XORWOW, (U - 0.5) * exp(0.5 * N(0,1)), seed 123456,
-A and B identical as in GEMMul8/testing/test_double.cu:273-274).
+Workloads (BASELINE.json configs):
+  cfg2 (default at --gpus 1)  DGEMM emulation m = n = k = 8192, num_moduli = 14, fast mode, 1 GPU
+  cfg3 (default at --gpus N>1) DGEMM emulation m = n = k = 16384, num_moduli = 14, fast mode, the
+                               (modulus, column block) units sharded over N GPUs (gemmul8.dist.gemm_moduli):
+                               strong scaling of ONE product, C left distributed by column blocks
+  cfg4                         mixed FP64 * FP32 -> FP64, 8192^3, num_moduli = 10, accurate mode, 1 GPU
+  cfg5                         complex DGEMM (COMPLEX_BIG_MATRIX_ENCODE), 4096^3, num_moduli = 12, 1 GPU
+Inputs come from the reference driver's generator (hiprand XORWOW, (U - 0.5) * exp(0.5 * N(0,1)),
+seed 123456, A and B identical for square shapes as in GEMMul8/testing/test_double.cu:273-274),
+NN, alpha = 1, beta = 0.  One "step" = one emulated GEMM with the operands resident in HBM.
+TFLOP/s = 2 m n k / time (8 m n k complex; test_double.cu:440).
 
-One "step" = one gemmul8 DGEMM call (scaling -> N int8 products -> CRT) with the
-operands resident in HBM.  TFLOP/s = 2*m*n*k / time (test_double.cu:440).
-
-Multi-GPU (torchrun, one process per GPU, RCCL), --partition:
-  rows (default)  weak scaling by output row blocks -- rank r computes the 8192-row
-                  block r of C = A * B for an (8192*N) x 8192 x 8192 product; B is
-                  replicated, no data-path collective (fast-mode shifts of a row depend
-                  only on that row, so the blocks are bit-identical to a single-GPU run
-                  of the whole product; gemmul8/dist.py).
-  moduli          strong scaling of ONE m=n=k=size product: rank r computes the residue
-                  planes of its moduli and sends them to rank 0 (P2P over xGMI), which
-                  runs the CRT (gemmul8.dist.matmul_moduli).
+--gpus N without a torchrun environment re-launches itself under torch.distributed.run with N
+ranks (one process per GPU, RCCL) before touching the GPU.  --partition rows selects the weak-scaling
+row-block partition instead (rank r: the 8192-row block r of an (8192 N) x 8192 x 8192 product).
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
+import sys
 import time
 
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
-import sys  # noqa: E402
-
 sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd"))
 
 INT8_PEAK_TOPS = 2048 * 4 * 256 * 2.4e9 / 1e12  # v_mfma_i32_32x32x32_i8: 2048 ops/clk/SIMD, 4 SIMD x 256 CU @ 2.4 GHz
 HBM_PEAK_GBS = 8000.0
 GH200_PUBLISHED_TFLOPS = 72.13  # OS2-fast-14 8192 on GH200 (R/...GH200...csv:192)
+BASELINE_METRIC = "emulated DGEMM TFLOP/s + max rel-error, m=n=k=8192 num_moduli=14"
+
+WORKLOADS = {
+    "cfg2": dict(size=8192, moduli=14, accurate=False, kind="d",
+                 text="cfg2: DGEMM emulation m=n=k=8192, num_moduli=14, fast mode, NN, alpha=1 beta=0"),
+    "cfg3": dict(size=16384, moduli=14, accurate=False, kind="d",
+                 text="cfg3: DGEMM emulation m=n=k=16384, num_moduli=14, fast mode, moduli sharded over the GPUs"),
+    "cfg4": dict(size=8192, moduli=10, accurate=True, kind="dfd",
+                 text="cfg4: mixed FP64*FP32->FP64 m=n=k=8192, num_moduli=10, accurate mode"),
+    "cfg5": dict(size=4096, moduli=12, accurate=False, kind="z",
+                 text="cfg5: complex DGEMM (COMPLEX_BIG_MATRIX_ENCODE) m=n=k=4096, num_moduli=12, fast mode"),
+}
 
 
 def parse():
@@ -43,10 +55,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--size", type=int, default=8192)
-    ap.add_argument("--moduli", type=int, default=14)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
+                    help="default: cfg2 on one GPU, cfg3 on more")
+    ap.add_argument("--size", type=int, default=None, help="override m = n = k")
+    ap.add_argument("--moduli", type=int, default=None)
     ap.add_argument("--accurate", action="store_true")
-    ap.add_argument("--partition", choices=["rows", "moduli"], default="rows")
+    ap.add_argument("--partition", choices=["moduli", "rows"], default="moduli")
+    ap.add_argument("--gather", action="store_true", help="moduli partition: collect C on rank 0 in the step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--no-dgemm", action="store_true")
@@ -54,10 +69,31 @@ def parse():
     return ap.parse_args()
 
 
-def dist_setup(args):
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def maybe_launch(args):
+    """--gpus N > 1 outside torchrun: run N ranks under torch.distributed.run as a child (no GPU touched
+    in this process) and exit with its status."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd, env=env))
+
+
+def dist_setup():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = None
     if world > 1:
         import torch.distributed as dist
         # one GPU per rank; GEMMUL8_BENCH_BACKEND=gloo (with ranks sharing a device) rehearses the
@@ -69,9 +105,11 @@ def dist_setup(args):
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     else:
         torch.cuda.set_device(0)
-    return world, rank
+    return world, rank, backend
 
 
 def barrier(world):
@@ -81,7 +119,7 @@ def barrier(world):
     torch.cuda.synchronize()
 
 
-def max_over_ranks(x, world):
+def reduce_max(x, world):
     if world == 1:
         return x
     import torch.distributed as dist
@@ -91,30 +129,54 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-def cpu_baseline(size_hint):
-    """The oracle (CPU restatement, OpenMP) timed on a bounded sample of the same workload."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown CPU"
+
+
+def cpu_baseline(size_hint, dev):
+    """The oracle (CPU restatement, OpenMP) timed on a bounded sample of the cfg2 workload (same generator,
+    fast mode, N = 14) and cfg1 (SGEMM emulation 1024^3, N = 4, fast) in full, both on this host."""
     import numpy as np
+    import gemmul8 as G
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     threads = O.num_threads()
     n = size_hint or 5120  # about 14 s of the oracle on 16 host threads (6.9 s at 4096)
-    rng = np.random.default_rng(123456)
-    A = np.asfortranarray((1.0 - rng.random((n, n)) - 0.5) * np.exp(0.5 * rng.standard_normal((n, n))))
+    A = G.randmat(n, n, torch.float64, 0.5, 123456, dev).cpu().numpy().T  # column-major n x n (F order)
     t0 = time.perf_counter()
-    O.gemm(A, A, 14, True)
+    C = O.gemm(A, A, 14, True)
     dt = time.perf_counter() - t0
-    model = "unknown CPU"
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
-    return {"value": 2.0 * n ** 3 / dt / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
-            "sample": f"DGEMM emulation m=n=k={n}, num_moduli=14, fast mode, one call ({dt:.1f} s) of the "
-                      f"oracle/oz2_oracle.c restatement with {threads} OpenMP threads on {model} "
-                      f"({os.cpu_count()} logical CPUs visible)"}
+    ref = A @ A
+    rel = np.abs(C - ref) / np.abs(ref)
+    out = {"value": 2.0 * n ** 3 / dt / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
+           "sample": f"cfg2 workload at m=n=k={n} (DGEMM emulation, num_moduli=14, fast mode, reference "
+                     f"generator seed 123456, A == B), one call ({dt:.1f} s) of the oracle/oz2_oracle.c "
+                     f"restatement with {threads} OpenMP threads on {_cpu_model()} ({os.cpu_count()} logical "
+                     f"CPUs visible)",
+           "relerr_max_vs_fp64": float(rel.max()), "relerr_median_vs_fp64": float(np.median(rel))}
+    # cfg1 in full: SGEMM emulation 1024^3, N = 4, fast mode (BASELINE.json configs[0])
+    A1 = G.randmat(1024, 1024, torch.float32, 0.5, 123456, dev).cpu().numpy().T
+    t0 = time.perf_counter()
+    C1 = O.gemm(A1, A1, 4, True)
+    dt1 = time.perf_counter() - t0
+    r1 = A1.astype(np.float64) @ A1.astype(np.float64)
+    rel1 = np.abs(C1.astype(np.float64) - r1) / np.abs(r1)
+    cfg1 = {"workload": "cfg1: SGEMM emulation m=n=k=1024, num_moduli=4, fast mode (CPU, full size)",
+            "seconds": round(dt1, 3), "tflops": 2.0 * 1024 ** 3 / dt1 / 1e12, "threads": threads,
+            "relerr_max_vs_fp64": float(rel1.max()), "relerr_median_vs_fp64": float(np.median(rel1)),
+            "sha256_C": hashlib.sha256(np.asfortranarray(C1).tobytes()).hexdigest()}
+    fx = os.path.join(ROOT, "tests", "golden", "cfg1_ref.json")
+    if os.path.exists(fx):
+        ref1 = json.load(open(fx))
+        cfg1["matches_reference_build"] = cfg1["sha256_C"] == ref1.get("sha256_C_reference")
+    out["cfg1"] = cfg1
+    return out
 
 
 def traffic_from_profile(shape):
@@ -132,44 +194,53 @@ def traffic_from_profile(shape):
     return t.get("gemm_hbm_bytes_per_launch")
 
 
+def make_operands(kind, m, n, k, seed_a, dev):
+    """column-major operands ((cols, rows) tensors) of the workload kind"""
+    import gemmul8 as G
+    if kind == "z":
+        return (G.randmat(m, k, torch.complex128, 0.5, seed_a, dev), G.randmat(k, n, torch.complex128, 0.5, 123456, dev),
+                torch.complex128)
+    tb = torch.float32 if kind == "dfd" else torch.float64
+    return G.randmat(m, k, torch.float64, 0.5, seed_a, dev), G.randmat(k, n, tb, 0.5, 123456, dev), torch.float64
+
+
 def main():
     args = parse()
-    world, rank = dist_setup(args)
+    maybe_launch(args)
+    world, rank, backend = dist_setup()
     import gemmul8 as G
+    from gemmul8 import dist as GD
 
-    m = n = k = args.size
-    N = args.moduli
+    wl_name = args.workload or ("cfg3" if (world > 1 and args.partition == "moduli") else "cfg2")
+    wl = WORKLOADS[wl_name]
+    m = n = k = args.size or wl["size"]
+    N = args.moduli or wl["moduli"]
+    fast = not (args.accurate or wl["accurate"])
+    kind = wl["kind"]
+    custom = (m != wl["size"] or N != wl["moduli"] or fast == wl["accurate"])
+    cplx = kind == "z"
+    ct = G.COMPLEX_BIG_MATRIX_ENCODE if cplx else G.REAL_DEFAULT
+    flop_per = (8.0 if cplx else 2.0) * m * n * k
     dev = torch.device("cuda", torch.cuda.current_device())
-    if args.partition == "moduli" and world > 1:
-        from gemmul8 import dist as GD
-        # row-major m x k / k x n operands (randmat(k, m) is the column-major k x m matrix)
-        Arm = G.randmat(k, m, torch.float64, 0.5, 123456, dev)
-        Brm = G.randmat(n, k, torch.float64, 0.5, 654321, dev)
-        A = B = None
+    sharded = world > 1 and args.partition == "moduli"
+    seed = 123456 + (rank if (world > 1 and not sharded) else 0)
+    A, B, tc = make_operands(kind, m, n, k, seed, dev)
+    trace = None
+    if sharded:
+        ops = GD.HipShardOps()
+        plan = GD.ShardPlan(m, n, N, world)
+        trace = []
 
-        def step():
-            GD.matmul_moduli(Arm, Brm, N, not args.accurate)
+        def step(tr=None):
+            return GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, tc, ct, gather=args.gather, ops=ops,
+                                  trace=tr)
     else:
-        # inputs (column-major; the (k, m) row-major tensor holds the column-major m x k matrix)
-        seed = 123456 + rank
-        A = G.randmat(m, k, torch.float64, 0.5, seed, dev)
-        B = G.randmat(k, n, torch.float64, 0.5, 123456, dev)
-        C = torch.empty((n, m), dtype=torch.float64, device=dev)
-        work = G.alloc_work(m, n, k, N, G.REAL_DEFAULT, dev)
+        C = torch.empty((n, m), dtype=tc, device=dev)
+        work = G.alloc_work(m, n, k, N, ct, dev)
 
-        def step():
-            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, not args.accurate, work)
-
-        if args.accurate and world > 1:
-            # accurate mode couples B's column shifts to every row block: one MAX all-reduce of
-            # the bound product's column maxima per call (gemmul8.dist.matmul_rows)
-            from gemmul8 import dist as GD
-            Arm = G.randmat(k, m, torch.float64, 0.5, seed, dev)
-            Brm = G.randmat(n, k, torch.float64, 0.5, 123456, dev)
-            A = B = None
-
-            def step():
-                GD.matmul_rows(Arm, Brm, N, False)
+        def step(tr=None):
+            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, work, ct)
+            return C
 
     for _ in range(args.warmup):
         step()
@@ -178,36 +249,69 @@ def main():
     barrier(world)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(trace)
     barrier(world)
     dt = time.perf_counter() - t0
     G.timing_enable(False)
     phase_ms, _ = G.timing_read()
-    dt = max_over_ranks(dt, world)
+    dt = reduce_max(dt, world)
     ms_per_step = dt / args.steps * 1e3
-    flops = 2.0 * m * n * k
-    strong = args.partition == "moduli" and world > 1
-    value = flops * (1 if strong else world) * args.steps / dt / 1e12
+    # strong scaling (one product over all ranks) or weak (row partition: one product per rank)
+    value = flop_per * (1 if (sharded or world == 1) else world) * args.steps / dt / 1e12
 
-    out = None
-    if rank == 0:
-        # per step: one gemm call (single GPU, row blocks) or, in the modulus partition, one product
-        # launch per owned plane (gemmul8.dist.matmul_moduli; its split and CRT go through the phase
-        # entry points, which time the products only)
-        avg = [x / args.steps for x in phase_ms]
-        # dominant kernel: the int8 products (all of this rank's moduli per step)
-        gemm_ms = avg[1]
+    avg = [x / args.steps for x in phase_ms]
+    extra = {}
+    # int8 MACs per output element and modulus relative to m n k: 1 real, 4 complex big matrix, 3 Karatsuba
+    fmac = (3.0 if G.layout(m, n, k, N, ct)["nsub"] == 3 else 4.0) if cplx else 1.0
+    if sharded:
+        # dominant kernel: the int8 products of rank 0's units (one products_cols launch per merged unit)
+        ops_step = sum(2.0 * m * (c1 - c0) * k * fmac for _, c0, c1 in plan.launches[rank])
+        planes = sum(c1 - c0 for _, c0, c1 in plan.launches[rank]) / n
+        seg = {}
+        for i in range(0, len(trace), 6):
+            evs = trace[i:i + 6]
+            for (a, ea), (b, eb) in zip(evs, evs[1:]):
+                seg[b] = seg.get(b, 0.0) + ea.elapsed_time(eb)
+        extra["step_phases_ms_rank0"] = {kk: round(v / args.steps, 4) for kk, v in seg.items()}
+        extra["units_rank0"] = [list(u) for u in plan.launches[rank]]
+    else:
+        ops_step = 2.0 * fmac * m * n * k * N
         planes = N
-        if strong:
-            from gemmul8 import dist as GD
-            a, b = GD.moduli_partition(N, world)[0]
-            planes = b - a  # rank 0's share of the moduli
-        ops = 2.0 * m * n * k * planes
-        achieved = ops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
-        roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(INT8_PEAK_TOPS, 1),
-                    "unit": "TFLOP/s", "frac": round(achieved / INT8_PEAK_TOPS, 4), "traffic": traffic_from_profile((m, n, k, planes, not args.accurate)),
-                    "kernel": "gemm_i8_persistent_kernel (residue products; int8 ops counted as FLOP, 2*m*n*k*num_moduli per launch)",
-                    "avg_launch_ms": round(gemm_ms, 4)}
+    gemm_ms = avg[1]
+    achieved = ops_step / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(INT8_PEAK_TOPS, 1), "unit": "TFLOP/s",
+                "frac": round(achieved / INT8_PEAK_TOPS, 4),
+                "traffic": traffic_from_profile((m, n, k, planes, fast)) if not cplx else None,
+                "kernel": G.last_products_kernel() + " (residue products; int8 ops counted as FLOP, "
+                          "2*m'*n'*k' per plane and launch" + (", rank 0's units)" if sharded else ")"),
+                "avg_launch_ms": round(gemm_ms, 4)}
+
+    # accuracy against a double-double reference (testing/eval.hpp semantics); sharded: each rank checks
+    # its own output columns, the max is combined
+    if not args.no_accuracy and not cplx and kind == "d":
+        Cout = step()
+        torch.cuda.synchronize()
+        if sharded:
+            c0, c1 = plan.cols[rank]
+            if args.gather:
+                Cout = None if rank else Cout[c0:c1]
+            if c1 > c0 and Cout is not None:
+                C1, C2 = G.dd_gemm(A, B[c0:c1], m, c1 - c0, k)
+                emax, emed = G.relerr_dd(Cout, C1, C2)
+                del C1, C2
+            else:
+                emax, emed = 0.0, 0.0
+            emax = reduce_max(emax, world)
+            extra["relerr_max"] = emax
+            extra["relerr_median_rank0_columns"] = emed
+        elif world == 1 or rank == 0:
+            C1, C2 = G.dd_gemm(A, B, m, n, k)
+            emax, emed = G.relerr_dd(Cout, C1, C2)
+            extra["relerr_max"] = emax
+            extra["relerr_median"] = emed
+            del C1, C2
+
+    if rank == 0:
         # measured live after the timed region: the same MFMA alone on uniformly random operand bytes
         # (the residue distribution) in registers -- the clock the chip holds under that load bounds
         # any int8 GEMM on such data
@@ -215,34 +319,34 @@ def main():
         if ceiling > 0:
             roofline["data_bound_ceiling"] = round(ceiling, 1)
             roofline["frac_of_data_bound_ceiling"] = round(achieved / ceiling, 4)
-        extra = {"phase_ms": {"scaling": round(avg[0], 4), "int8_products": round(avg[1], 4),
-                              "inverse_scaling": round(avg[3], 4)}}
-        if not args.no_accuracy and A is not None:
-            # accuracy against a double-double reference (testing/eval.hpp semantics)
-            step()
-            torch.cuda.synchronize()
-            C1, C2 = G.dd_gemm(A, B, m, n, k)
-            emax, emed = G.relerr_dd(C, C1, C2)
-            extra["relerr_max"] = emax
-            extra["relerr_median"] = emed
-            del C1, C2
-        if not args.no_dgemm and A is not None:
-            Ar = A.t()  # logical m x k view
-            Br = B.t()
+        if not sharded:
+            extra["phase_ms"] = {"scaling": round(avg[0], 4), "int8_products": round(avg[1], 4),
+                                 "inverse_scaling": round(avg[3], 4)}
+        if not args.no_dgemm and kind == "d" and (world == 1 or sharded):
+            # the vendor DGEMM of the same shape on ONE GPU (rocBLAS through torch)
+            Ar, Br = A.t(), B.t()
             for _ in range(2):
                 torch.matmul(Ar, Br)
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            reps = 5
+            reps = 5 if m <= 8192 else 2
             for _ in range(reps):
                 torch.matmul(Ar, Br)
             torch.cuda.synchronize()
-            dg = flops * reps / (time.perf_counter() - t1) / 1e12
-            extra["rocblas_dgemm_tflops"] = round(dg, 2)
-            extra["vs_rocblas_dgemm"] = round(value / world / dg, 3)
-        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(args.cpu_sample)
+            dg = 2.0 * m * n * k * reps / (time.perf_counter() - t1) / 1e12
+            extra["rocblas_dgemm_tflops_1gpu"] = round(dg, 2)
+            extra["vs_rocblas_dgemm_1gpu"] = round(value / dg, 3)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev)
+        if custom:
+            workload = (f"{'complex ' if cplx else ''}{'mixed ' if kind == 'dfd' else ''}DGEMM emulation m=n=k={m}, "
+                        f"num_moduli={N}, {'fast' if fast else 'accurate'} mode")
+        else:
+            workload = wl["text"]
+        metric = BASELINE_METRIC if (wl_name == "cfg2" and not custom) else \
+            f"emulated {'ZGEMM' if cplx else 'DGEMM'} TFLOP/s + max rel-error, m=n=k={m} num_moduli={N}" + \
+            ("" if fast else " accurate") + (f" ({wl_name})" if not custom else "")
         out = {
-            "metric": "emulated DGEMM TFLOP/s + max rel-error, m=n=k=8192 num_moduli=14",
+            "metric": metric,
             "value": round(value, 3),
             "unit": "TFLOP/s",
             "n_gpus": world,
@@ -250,18 +354,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
-            "vs_baseline": round(value / world / GH200_PUBLISHED_TFLOPS, 3),
+            "scaling": "strong" if sharded else "weak",
+            "vs_baseline": round(value / world / GH200_PUBLISHED_TFLOPS, 3) if (wl_name == "cfg2" and not custom) else None,
             "vs_baseline_ref": "GH200 published OS2-fast-14 8192 (72.13 TFLOP/s, BASELINE.md); per-GPU ratio",
             "dtype": "i8",
-            "io_dtype": "f64",
-            "data": "synthetic: hiprand XORWOW (U-0.5)*exp(0.5*N(0,1)), seed 123456 (rank r: A seed 123456+r), "
-                    "A == B at N=1 as in the reference driver",
-            "config": {"workload": "cfg2: DGEMM emulation m=n=k=8192, num_moduli=14, fast mode, NN, alpha=1 beta=0"
-                       if (m == 8192 and N == 14 and not args.accurate) else
-                       f"DGEMM emulation m=n=k={m}, num_moduli={N}, {'accurate' if args.accurate else 'fast'} mode",
-                       "m": m, "n": n, "k": k, "num_moduli": N, "fastmode": not args.accurate,
-                       "parallelism": (f"{args.partition} x{world}" if world > 1 else "single")},
+            "io_dtype": {"d": "f64", "dfd": "f64*f32->f64", "z": "c128"}[kind],
+            "data": "synthetic: hiprand XORWOW (U-0.5)*exp(0.5*N(0,1)), seed 123456, A == B as in the reference "
+                    "driver" + (" (row partition: rank r's A seed 123456+r)" if (world > 1 and not sharded) else ""),
+            "config": {"workload": workload, "m": m, "n": n, "k": k, "num_moduli": N, "fastmode": fast,
+                       "parallelism": (("moduli x column blocks" if sharded else "rows") + f" x{world}")
+                       if world > 1 else "single",
+                       "world_size": world, "backend": backend or "none",
+                       "output": ("C gathered on rank 0" if args.gather else "C distributed by column blocks")
+                       if sharded else "C on each rank"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

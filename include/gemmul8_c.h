@@ -71,11 +71,17 @@ int gemmul8_gemm_lowmem(void *stream, int op_a, int op_b, size_t m, size_t n, si
  * Accurate mode couples the shifts of op(B)'s columns to every row of op(A) (the int8 bound
  * product's column maxima).  A row-block shard therefore runs gemmul8_split_bound, combines the
  * column maxima (int32 [n] at work + offBound + 4 * m_pad) with a MAX all-reduce, and calls
- * gemmul8_split with GEMMUL8_SPLIT_BOUND_READY. */
-enum { GEMMUL8_SPLIT_BOUND_READY = 1 };
+ * gemmul8_split with GEMMUL8_SPLIT_BOUND_READY.
+ *
+ * One workspace may serve several gemmul8_products / _products_cols launches in flight on
+ * different streams only when their mod_begin differ (each first modulus has its own tile-queue
+ * heads); launches ordered on one stream may share anything. */
+enum { GEMMUL8_SPLIT_BOUND_READY = 1, GEMMUL8_SPLIT_SHIFTS_READY = 2 };
 int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
                         int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
                         void *work, int compute_type);
+/* flags: GEMMUL8_SPLIT_BOUND_READY (accurate: bound maxima in the workspace, derive the shifts from
+ * them), GEMMUL8_SPLIT_SHIFTS_READY (sftA / sftB already in the workspace: encode the slices only) */
 int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b, int type_c,
                   const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli, int fastmode, void *work,
                   int compute_type, unsigned mod_begin, unsigned mod_end, int flags);
@@ -83,6 +89,37 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
                      unsigned mod_begin, unsigned mod_end);
 int gemmul8_recombine(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c, int compute_type,
                       const void *alpha, const void *beta, void *C, size_t ldc, void *work);
+
+/* --- sharded entry points (the moduli x column-block partition of gemmul8/dist.py) ---------------
+ * Every output element's CRT needs all N residues, and every residue plane is column-major
+ * (plane j, column c at work + offR + j * planeR + c * ldr), so a column range of a plane is one
+ * contiguous run of bytes.  A job over W ranks: (1) each rank computes the shifts of its own
+ * rows / columns (gemmul8_shard_stats), the ranks all-gather the int16 shift vectors into every
+ * workspace (offSftA / offSftB; accurate mode: sft0 at offSft0, A's rows then B's columns from
+ * bm_pad), accurate mode then runs gemmul8_shard_bound over its column range and MAX-all-reduces
+ * the bound area (int32 [bm_pad + n_pad] at offBound); (2) gemmul8_split(..., SHIFTS_READY or
+ * BOUND_READY) encodes its moduli; (3) gemmul8_products_cols produces its (modulus, column-range)
+ * units; (4) the ranks exchange the residue column runs so each holds all N planes of its own
+ * output columns; (5) gemmul8_recombine_cols.  Row / column range starts are multiples of 256
+ * (the product tile) for products_cols / shard_bound; range ends are multiples of 256 or n.
+ * The result is bit-identical to gemmul8_gemm on the same operands. */
+/* fast mode: sftA[row_begin, row_end) and sftB[col_begin, col_end); accurate mode: the sft0 of the same ranges */
+int gemmul8_shard_stats(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
+                        int fastmode, void *work, int compute_type, size_t row_begin, size_t row_end,
+                        size_t col_begin, size_t col_end);
+/* accurate mode, sft0 assembled: magnitude planes + the bound product over columns [col_begin, col_end)
+ * (the bound area is zeroed first; the other columns' maxima stay 0) */
+int gemmul8_shard_bound(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
+                        void *work, int compute_type, size_t col_begin, size_t col_end);
+/* residue planes [mod_begin, mod_end), columns [col_begin, col_end) only (one launch) */
+int gemmul8_products_cols(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type,
+                          void *work, unsigned mod_begin, unsigned mod_end, size_t col_begin, size_t col_end);
+/* CRT + scaling + epilogue of the output columns [col_begin, col_end); C points at column col_begin */
+int gemmul8_recombine_cols(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c,
+                           int compute_type, const void *alpha, const void *beta, void *C, size_t ldc, void *work,
+                           size_t col_begin, size_t col_end);
 
 /* --- instrumentation (used by bench.py / tests) --------------------------------------------- */
 /* When enabled, every gemmul8_gemm records HIP events between its phases on its stream; the
@@ -111,6 +148,10 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
  * mismatching (input, modulus) pairs (0 expected; path 2 is a negative control that compares path 0
  * with a wrong expectation, so every pair mismatches). */
 unsigned long long gemmul8_residue_selftest(void *stream, int path);
+
+/* Name of the residue-product kernel the last products launch of this process took
+ * ("gemm_i8_persistent_kernel", "gemm_i8_kernel", "gemm_i8_kernel (k-chunked)" or "none"). */
+const char *gemmul8_last_products_kernel(void);
 
 /* --- bench / test harness (not part of the emulation path) ------------------------------------ */
 /* The reference's input generator (testing/make_matrix.hpp:8-71): x = (U(0,1] - 0.5) * exp(phi * N(0,1))

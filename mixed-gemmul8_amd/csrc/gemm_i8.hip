@@ -25,6 +25,8 @@
 // Operand panels (16 KiB, pre-arranged in fragment order by split.hip) stream
 // HBM -> LDS through a 4-slot ring (128 KiB) with LDS-DMA issued three k-steps
 // ahead; waits are counted by hand (vmcnt), barriers are raw s_barrier.
+#include <atomic>
+
 #include "oz2_split.hpp"
 
 namespace oz2 {
@@ -909,18 +911,23 @@ unsigned long long residue_selftest(int path, hipStream_t st) {
     return h;
 }
 
-// CUs of the current device (one persistent block each)
+// CUs of the current device (one persistent block each); cached per device id below 64 (atomics: any
+// host thread may launch), queried on every call beyond
 static unsigned device_cu_count() {
-    static unsigned cached[64] = {};
+    static std::atomic<unsigned> cached[64] = {};
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (!cached[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cached[dev] = (unsigned)n;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+    if (dev < 64) {
+        const unsigned c = cached[dev].load(std::memory_order_relaxed);
+        if (c) return c;
     }
-    return cached[dev];
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+    if (dev < 64) cached[dev].store((unsigned)n, std::memory_order_relaxed);
+    return (unsigned)n;
 }
+// the residue-product kernel the last gemm_i8 RESIDUE launch of this process took (bench.py labels)
+std::atomic<int> g_last_residue_kernel{0};
 // GEMMUL8_PERSISTENT: 0 = one-tile kernel only, 1 = persistent kernel wherever it applies, unset =
 // persistent when the launch has at least three tiles per CU.  g_persistent_override (probes) wins when >= 0.
 int g_persistent_override = -1;
@@ -985,6 +992,7 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     }();
     const unsigned chunk = forced_chunk ? forced_chunk : ((1u << 16) / KSTEP);
     if (epi == Epi::RESIDUE && (L.k_pad > ((size_t)1 << 17) || (forced_chunk && g.ksteps > forced_chunk))) {
+        g_last_residue_kernel.store(3, std::memory_order_relaxed);
         g.biased = 1;
         for (unsigned k0 = 0; k0 < g.kstride; k0 += chunk) {
             g.k0 = k0;
@@ -1004,6 +1012,7 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     const unsigned ncu = device_cu_count();
     const int pmode = persistent_mode();
     if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 3 * ncu)) {
+        g_last_residue_kernel.store(2, std::memory_order_relaxed);
         g.nplanes = nplanes * g.nsub;
         g.queue = queue;
         g.stamps = g_stamps;
@@ -1028,7 +1037,10 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         return;
     }
     switch (epi) {
-    case Epi::RESIDUE: buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0); break;
+    case Epi::RESIDUE:
+        g_last_residue_kernel.store(1, std::memory_order_relaxed);
+        buf ? OZ2_GEMM(0, 1) : OZ2_GEMM(0, 0);
+        break;
     case Epi::BOUND: buf ? OZ2_GEMM1(1, 1) : OZ2_GEMM1(1, 0); break;
     default: buf ? OZ2_GEMM1(2, 1) : OZ2_GEMM1(2, 0); break;
     }

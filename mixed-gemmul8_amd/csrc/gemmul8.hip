@@ -243,6 +243,9 @@ static Views views(void *work, size_t m, size_t n, size_t k, unsigned N, bool cp
     return v;
 }
 
+// tile-queue heads of a products launch whose first modulus is j0 (oz2_common.hpp make_layout)
+static inline uint32_t *queue_of(const Views &v, unsigned j0) { return v.queue + QUEUE_HEADS * j0; }
+
 // moduli [j0, j1) of an N-moduli call, renumbered from 0 (plane pointers are offset by the caller)
 static ModParams sub_mod_params(unsigned N, unsigned j0, unsigned j1) {
     const ModParams full = make_mod_params(N);
@@ -259,21 +262,32 @@ static ModParams sub_mod_params(unsigned N, unsigned j0, unsigned j1) {
 
 // accurate mode, first half of phase 1: sft0 = 5 - ilogb(amax), the 6-bit magnitude planes and the
 // bound product's row / column maxima (scaling.hpp:3053-3100).  A on the call's stream, B on the lane.
-static void phase_bound(const Call &c, const Views &v) {
+// Sharded form (gemmul8_shard_bound): sft0 already assembled in the workspace (sft0_ready) and the
+// bound product restricted to the columns [c0, c1) of op(B) (c0 a multiple of TILE): the column maxima
+// outside the range stay 0 and the row maxima cover those columns only, so a MAX all-reduce of the
+// bound area over ranks holding complementary ranges gives the whole product's maxima.
+static void phase_bound(const Call &c, const Views &v, size_t c0 = 0, size_t c1 = SIZE_MAX, bool sft0_ready = false) {
     // always the big-matrix geometry (Karatsuba layouts size their slice regions to hold it)
     const Layout L = v.L.kara ? make_layout(c.m, c.n, c.k, c.N, c.cplx, v.L.S, 0) : v.L;
     const ModParams MP = make_mod_params(c.N);
     fork(c);
-    split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
+    if (!sft0_ready) split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
     split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
-    split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.stB);
+    if (!sft0_ready) split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.stB);
     // big-matrix B magnitudes carry the reference's tail defect; classic / Karatsuba do not
     // the B tail defect lives in the op-N big-matrix extraction only (scaling.hpp:2312-2323, 3201-3203)
     split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.stB,
                  c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE && c.B.contig);
     join(c);
     zero_i32(v.bound, L.m_pad + L.n_pad, c.st);
-    gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
+    if (c1 > c.n) c1 = c.n;
+    if (c0 == 0 && c1 == c.n) {
+        gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
+    } else if (c0 < c1) {
+        const size_t t0 = c0 / TILE, t1 = (c1 + TILE - 1) / TILE;
+        gemm_i8(v.A8, v.B8 + t0 * L.ksteps * PANEL, col_tiles(L, t0, t1), 1, Epi::BOUND, nullptr, v.bound,
+                v.bound + L.m_pad + t0 * TILE, MP, c.st);
+    }
 }
 
 // phase 1a: shifts of every row of op(A) (is_A) or column of op(B), shared by all moduli
@@ -296,27 +310,29 @@ static void operand_encode(const Call &c, const Views &v, bool is_A, unsigned j0
                            hipStream_t st) {
     const Layout &L = v.L;
     ModParams SP = sub_mod_params(c.N, j0, j1);
-    SP.zero_queue = is_A ? v.queue : nullptr;  // the products that follow find their tile queue zeroed
+    SP.zero_queue = is_A ? queue_of(v, j0) : nullptr;  // the products that follow find their tile queue zeroed
     if (is_A) split_encode(c.A, true, c.m, c.k, v.sftA, v.A8 + slot * L.planeA, L.planeA, L, 0, SP, st);
     else split_encode(c.B, false, c.n, c.k, v.sftB, v.B8 + slot * L.planeB, L.planeB, L, 0, SP, st);
 }
 
 // phase 1 (shifts + slices of moduli [j0, j1) into their own planes); bound_ready: accurate mode
 // takes the row / column maxima already in the workspace (phase_bound, possibly combined across
-// row blocks)
-static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1, bool bound_ready) {
-    if (!c.fast && !bound_ready) phase_bound(c, v);
+// row blocks); shifts_ready: sftA / sftB are already in the workspace (assembled from the shards
+// of gemmul8_shard_stats), only the slices are encoded
+static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1, bool bound_ready,
+                        bool shifts_ready = false) {
+    if (!c.fast && !bound_ready && !shifts_ready) phase_bound(c, v);
     if (!c.lane) {
         // one stream (small problems): both operands' shifts, then both operands' slices, one launch each
         // where the operand forms allow it
-        if (!(c.fast && split_stats_pair(c.A, c.m, c.B, c.n, c.k, c.VT, oz2_log2M_fast[c.N - 2], v.sftA, v.sftB,
-                                         c.st))) {
+        if (!shifts_ready && !(c.fast && split_stats_pair(c.A, c.m, c.B, c.n, c.k, c.VT, oz2_log2M_fast[c.N - 2],
+                                                          v.sftA, v.sftB, c.st))) {
             operand_shifts(c, v, true, c.st);
             operand_shifts(c, v, false, c.st);
         }
         const Layout &L = v.L;
         ModParams SP = sub_mod_params(c.N, j0, j1);
-        SP.zero_queue = v.queue;
+        SP.zero_queue = queue_of(v, j0);
         if (split_encode_pair(c.A, c.m, c.B, c.n, c.k, v.sftA, v.sftB, v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB, L,
                               SP, c.st))
             return;
@@ -325,9 +341,9 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
         return;
     }
     fork(c);
-    operand_shifts(c, v, true, c.st);
+    if (!shifts_ready) operand_shifts(c, v, true, c.st);
     operand_encode(c, v, true, j0, j1, j0, c.st);
-    operand_shifts(c, v, false, c.stB);
+    if (!shifts_ready) operand_shifts(c, v, false, c.stB);
     operand_encode(c, v, false, j0, j1, j0, c.stB);
     join(c);
 }
@@ -339,14 +355,41 @@ static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1,
                            bool queue_zeroed) {
     const Layout &L = v.L;
     gemm_i8(v.A8 + slot * L.planeA, v.B8 + slot * L.planeB, L, j1 - j0, Epi::RESIDUE, v.R + j0 * L.planeR, nullptr,
-            nullptr, sub_mod_params(N, j0, j1), st, v.queue, queue_zeroed);
+            nullptr, sub_mod_params(N, j0, j1), st, queue_of(v, j0), queue_zeroed);
 }
 
-// phase 3: CRT + scaling + BLAS epilogue over all N residue planes
+// phase 3: CRT + scaling + BLAS epilogue over all N residue planes; columns [c0, c1) of the output only
+// when given (C then points at column c0): the residue planes are column-major, so a column range is
+// the same kernel over an offset plane base, sftB + c0 and n = c1 - c0
 static void phase_crt(const Views &v, unsigned N, OutType ot, const void *alpha, const void *beta, void *C, size_t ldc,
-                      hipStream_t st) {
+                      hipStream_t st, size_t c0 = 0, size_t c1 = SIZE_MAX) {
     const CrtParams CP = make_crt_params(N, ot == OutType::F32 || ot == OutType::C32);
-    crt_inverse(v.R, v.L, v.sftA, v.sftB, CP, ot, alpha, beta, C, ldc, st);
+    if (c0 == 0 && c1 >= v.L.n) {
+        crt_inverse(v.R, v.L, v.sftA, v.sftB, CP, ot, alpha, beta, C, ldc, st);
+        return;
+    }
+    Layout L = v.L;
+    L.n = c1 - c0;
+    crt_inverse(v.R + c0 * L.ldr, L, v.sftA, v.sftB + c0, CP, ot, alpha, beta, C, ldc, st);
+}
+
+// phase 2 over the columns [c0, c1) of the residue planes only (c0 a multiple of TILE, c1 one too or n):
+// the B slice tiles and the residue columns of that range, every row
+static void phase_products_cols(const Views &v, unsigned N, unsigned j0, unsigned j1, size_t c0, size_t c1,
+                                hipStream_t st) {
+    const Layout &L = v.L;
+    const size_t t0 = c0 / TILE, t1 = (c1 + TILE - 1) / TILE;
+    gemm_i8(v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB + t0 * L.ksteps * PANEL, col_tiles(L, t0, t1), j1 - j0,
+            Epi::RESIDUE, v.R + j0 * L.planeR + t0 * TILE * L.ldr, nullptr, nullptr, sub_mod_params(N, j0, j1), st,
+            queue_of(v, j0), false);
+}
+
+// operand descriptor of the vectors [v0, ...) of d (rows of op(A) / columns of op(B))
+static OperandDesc sub_operand(const OperandDesc &d, size_t v0) {
+    OperandDesc s = d;
+    const size_t es = (d.dbl ? 8 : 4) * (d.cplx ? 2 : 1);
+    s.ptr = static_cast<const char *>(d.ptr) + (d.contig ? v0 * d.ld : v0) * es;
+    return s;
 }
 
 static int run(Call &c, double *phase_ns) {
@@ -548,15 +591,22 @@ int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k
     oz2::clear_stale_error();
     oz2::LaneGuard lane(c);
     oz2::phase_split(c, oz2::views(work, m, n, k, num_moduli, c.cplx), mod_begin, mod_end,
-                     (flags & GEMMUL8_SPLIT_BOUND_READY) != 0);
+                     (flags & GEMMUL8_SPLIT_BOUND_READY) != 0, (flags & GEMMUL8_SPLIT_SHIFTS_READY) != 0);
     return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
 
 int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type, void *work,
                      unsigned mod_begin, unsigned mod_end) {
+    return gemmul8_products_cols(stream, m, n, k, num_moduli, compute_type, work, mod_begin, mod_end, 0, n);
+}
+
+int gemmul8_products_cols(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int compute_type,
+                          void *work, unsigned mod_begin, unsigned mod_end, size_t col_begin, size_t col_end) {
     if (num_moduli < 2 || num_moduli > 20 || mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
     if (compute_type < GEMMUL8_REAL_DEFAULT || compute_type > GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_TYPES;
-    if (m == 0 || n == 0) return GEMMUL8_OK;
+    if (col_begin > col_end || col_end > n) return GEMMUL8_E_SIZE;
+    if (m == 0 || col_begin == col_end) return GEMMUL8_OK;
+    if (col_begin % oz2::TILE || (col_end != n && col_end % oz2::TILE)) return GEMMUL8_E_SIZE;
     oz2::clear_stale_error();
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, compute_type != GEMMUL8_REAL_DEFAULT);
     hipStream_t st = static_cast<hipStream_t>(stream);
@@ -572,7 +622,8 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
         }
     }
     oz2::timing::Phase prod(record, st, rec.prod0, rec.prod1);
-    oz2::phase_products(v, num_moduli, mod_begin, mod_end, mod_begin, st, false);
+    if (col_begin == 0 && col_end == n) oz2::phase_products(v, num_moduli, mod_begin, mod_end, mod_begin, st, false);
+    else oz2::phase_products_cols(v, num_moduli, mod_begin, mod_end, col_begin, col_end, st);
     prod.end();
     if (record) {
         std::lock_guard<std::mutex> g(oz2::timing::mu);
@@ -583,17 +634,69 @@ int gemmul8_products(void *stream, size_t m, size_t n, size_t k, unsigned num_mo
 
 int gemmul8_recombine(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c, int compute_type,
                       const void *alpha, const void *beta, void *C, size_t ldc, void *work) {
+    return gemmul8_recombine_cols(stream, m, n, k, num_moduli, type_c, compute_type, alpha, beta, C, ldc, work, 0, n);
+}
+
+int gemmul8_recombine_cols(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c,
+                           int compute_type, const void *alpha, const void *beta, void *C, size_t ldc, void *work,
+                           size_t col_begin, size_t col_end) {
     if (num_moduli < 2 || num_moduli > 20) return GEMMUL8_E_MODULI;
+    if (col_begin > col_end || col_end > n) return GEMMUL8_E_SIZE;
     if (type_c < 0 || type_c > 3) return GEMMUL8_E_TYPES;
     const bool cp = compute_type != GEMMUL8_REAL_DEFAULT;
     if (cp != oz2::dt_cplx(type_c)) return GEMMUL8_E_TYPES;
     if (compute_type < GEMMUL8_REAL_DEFAULT || compute_type > GEMMUL8_COMPLEX_KARATSUBA_MULT) return GEMMUL8_E_TYPES;
     if (ldc < m) return GEMMUL8_E_SIZE;
-    if (m == 0 || n == 0) return GEMMUL8_OK;
+    if (m == 0 || col_begin == col_end) return GEMMUL8_OK;
     oz2::clear_stale_error();
     const oz2::Views v = oz2::views(work, m, n, k, num_moduli, cp);
     oz2::phase_crt(v, num_moduli, static_cast<oz2::OutType>(type_c), alpha, beta, C, ldc,
-                   static_cast<hipStream_t>(stream));
+                   static_cast<hipStream_t>(stream), col_begin, col_end);
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_shard_stats(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
+                        int fastmode, void *work, int compute_type, size_t row_begin, size_t row_end,
+                        size_t col_begin, size_t col_end) {
+    oz2::Call c{};
+    const int rc = oz2::prepare(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, nullptr, A, lda, B, ldb, nullptr,
+                                nullptr, m, num_moduli, fastmode, work, compute_type, c);
+    if (rc != GEMMUL8_OK) return rc;
+    if (row_begin > row_end || row_end > m || col_begin > col_end || col_end > n) return GEMMUL8_E_SIZE;
+    const size_t rows = row_end - row_begin, cols = col_end - col_begin;
+    if (rows == 0 && cols == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
+    const oz2::Views v = oz2::views(work, m, n, k, num_moduli, c.cplx);
+    const oz2::OperandDesc a = oz2::sub_operand(c.A, row_begin), b = oz2::sub_operand(c.B, col_begin);
+    if (c.fast) {
+        const float log2M = oz2_log2M_fast[num_moduli - 2];
+        int16_t *sa = v.sftA + row_begin, *sb = v.sftB + col_begin;
+        if (!(rows && cols && oz2::split_stats_pair(a, rows, b, cols, k, c.VT, log2M, sa, sb, c.st))) {
+            if (rows) oz2::split_stats(a, k, rows, c.VT, false, log2M, sa, c.st);
+            if (cols) oz2::split_stats(b, k, cols, c.VT, false, log2M, sb, c.st);
+        }
+    } else {  // sft0 = 5 - ilogb(amax): A's rows at sft0[0, bm_pad), B's columns after them (phase_bound)
+        if (rows) oz2::split_stats(a, k, rows, c.VT, true, 0.f, v.sft0 + row_begin, c.st);
+        if (cols) oz2::split_stats(b, k, cols, c.VT, true, 0.f, v.sft0 + v.L.bm_pad + col_begin, c.st);
+    }
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_shard_bound(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                        int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
+                        void *work, int compute_type, size_t col_begin, size_t col_end) {
+    oz2::Call c{};
+    const int rc = oz2::prepare(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, nullptr, A, lda, B, ldb, nullptr,
+                                nullptr, m, num_moduli, 0, work, compute_type, c);
+    if (rc != GEMMUL8_OK) return rc;
+    if (col_begin > col_end || col_end > n) return GEMMUL8_E_SIZE;
+    if (col_begin != col_end && (col_begin % oz2::TILE || (col_end != n && col_end % oz2::TILE))) return GEMMUL8_E_SIZE;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
+    const oz2::Views v = oz2::views(work, m, n, k, num_moduli, c.cplx);
+    oz2::LaneGuard lane(c);
+    oz2::phase_bound(c, v, col_begin, col_end, true);
     return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
 
@@ -632,6 +735,15 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
     oz2::gemm_i8(base + L.offA, base + L.offB, L, 1, oz2::Epi::RAW, C32, nullptr, nullptr, MP,
                  static_cast<hipStream_t>(stream));
     return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+const char *gemmul8_last_products_kernel(void) {
+    switch (oz2::g_last_residue_kernel.load(std::memory_order_relaxed)) {
+    case 1: return "gemm_i8_kernel";
+    case 2: return "gemm_i8_persistent_kernel";
+    case 3: return "gemm_i8_kernel (k-chunked)";
+    default: return "none";
+    }
 }
 
 unsigned long long gemmul8_residue_selftest(void *stream, int path) {

@@ -33,6 +33,7 @@ namespace oz2 {
 constexpr int TILE = 256;          // vectors per panel (GEMM block tile edge)
 constexpr int KSTEP = 64;          // k-bytes per panel
 constexpr int PANEL = TILE * KSTEP;  // 16 KiB
+constexpr int QUEUE_HEADS = 8;       // tile-queue heads per products launch (one per XCD)
 
 enum class Scal : int { F64 = 0, F32 = 1 };
 
@@ -139,9 +140,20 @@ static inline Layout make_layout(size_t m, size_t n, size_t k, unsigned N, bool 
     L.offSftB = off; off += round_up(L.bn_pad * 2, 256);
     L.offBound = off; off += round_up((L.bm_pad + L.bn_pad) * 4, 256);
     L.offSft0 = off; off += round_up((L.bm_pad + L.bn_pad) * 2, 256);
-    L.offQueue = off; off += 256;  // 8 per-XCD tile-queue heads of the persistent product kernel
+    // 8 per-XCD tile-queue heads of the persistent product kernel, one set per first modulus of a
+    // products launch: launches of disjoint moduli ranges may share the workspace on different streams
+    L.offQueue = off; off += round_up(QUEUE_HEADS * OZ2_MAX_MODULI * 4, 256);
     L.total = off;
     return L;
+}
+
+// the products of one column range [t0, t1) of B's vector tiles (the residue planes' column
+// tiles): the same planes and strides, fewer column tiles.  gemm_i8's tile indices are relative,
+// so the caller offsets the B slice pointer by t0 * ksteps panels and the output by t0 * 256 * ldr.
+static inline Layout col_tiles(const Layout &L, size_t t0, size_t t1) {
+    Layout S = L;
+    S.ntiles = t1 - t0;
+    return S;
 }
 
 // byte offset of the 16-B chunk holding (vector v, k-bytes kk..kk+15), kk % 16 == 0

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_ext.h>
 
+#include <atomic>
+
 #include "oz2_common.hpp"
 
 namespace oz2 {
@@ -81,6 +83,9 @@ enum class Epi : int { RESIDUE = 0, BOUND = 1, RAW = 2 };
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
              int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue = nullptr,
              bool queue_zeroed = false);
+// the residue-product kernel of the last RESIDUE launch: 0 none yet, 1 one-tile (gemm_i8_kernel),
+// 2 persistent (gemm_i8_persistent_kernel), 3 k-chunked one-tile launches
+extern std::atomic<int> g_last_residue_kernel;
 // exhaustive exactness check of the residue epilogues (0 = biased, 1 = signed): mismatch count
 unsigned long long residue_selftest(int path, hipStream_t st);
 

@@ -44,6 +44,10 @@ def _load():
     lib.gemmul8_split_bound.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, sz, p, sz, u, p, i]
     lib.gemmul8_products.argtypes = [p, sz, sz, sz, u, i, p, u, u]
     lib.gemmul8_recombine.argtypes = [p, sz, sz, sz, u, i, i, p, p, p, sz, p]
+    lib.gemmul8_shard_stats.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, sz, p, sz, u, i, p, i, sz, sz, sz, sz]
+    lib.gemmul8_shard_bound.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, sz, p, sz, u, p, i, sz, sz]
+    lib.gemmul8_products_cols.argtypes = [p, sz, sz, sz, u, i, p, u, u, sz, sz]
+    lib.gemmul8_recombine_cols.argtypes = [p, sz, sz, sz, u, i, i, p, p, p, sz, p, sz, sz]
     lib.gemmul8_work_size_lowmem.restype = sz
     lib.gemmul8_work_size_lowmem.argtypes = [sz, sz, sz, u, i, u]
     lib.gemmul8_gemm_lowmem.restype = i
@@ -55,6 +59,8 @@ def _load():
     lib.gemmul8_randmat.argtypes = [p, i, sz, sz, p, ctypes.c_double, ctypes.c_ulonglong]
     lib.gemmul8_dd_gemm.argtypes = [p, sz, sz, sz, p, p, p, p]
     lib.gemmul8_relerr_dd.argtypes = [p, sz, p, p, p, p]
+    lib.gemmul8_last_products_kernel.restype = ctypes.c_char_p
+    lib.gemmul8_last_products_kernel.argtypes = []
     lib.gemmul8_mfma_ceiling.restype = ctypes.c_double
     lib.gemmul8_mfma_ceiling.argtypes = [p, i]
     return lib
@@ -135,15 +141,35 @@ def gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fas
 
 # ---- phase entry points (gemm == split + products + recombine; used by gemmul8.dist) ----
 SPLIT_BOUND_READY = 1
+SPLIT_SHIFTS_READY = 2
 
 
 def split(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, work, out_dtype, mod_begin=0, mod_end=None,
-          computeType=REAL_DEFAULT, stream=None, bound_ready=False):
-    """Shifts of op(A)/op(B) and the int8 slices of moduli [mod_begin, mod_end) into `work`."""
+          computeType=REAL_DEFAULT, stream=None, bound_ready=False, shifts_ready=False):
+    """Shifts of op(A)/op(B) and the int8 slices of moduli [mod_begin, mod_end) into `work`
+    (shifts_ready: the shifts are already in `work`, only the slices are encoded)."""
     mod_end = num_moduli if mod_end is None else mod_end
+    flags = (SPLIT_BOUND_READY if bound_ready else 0) | (SPLIT_SHIFTS_READY if shifts_ready else 0)
     _check(lib.gemmul8_split(_stream(stream), opA, opB, m, n, k, _DTYPE[A.dtype], _DTYPE[B.dtype], _DTYPE[out_dtype],
                              A.data_ptr(), lda, B.data_ptr(), ldb, num_moduli, int(bool(fastmode)), work.data_ptr(),
-                             computeType, mod_begin, mod_end, SPLIT_BOUND_READY if bound_ready else 0))
+                             computeType, mod_begin, mod_end, flags))
+
+
+def shard_stats(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, work, out_dtype, rows, cols,
+                computeType=REAL_DEFAULT, stream=None):
+    """Shifts (fast) or sft0 (accurate) of the rows [rows) of op(A) and the columns [cols) of op(B) into `work`."""
+    _check(lib.gemmul8_shard_stats(_stream(stream), opA, opB, m, n, k, _DTYPE[A.dtype], _DTYPE[B.dtype],
+                                   _DTYPE[out_dtype], A.data_ptr(), lda, B.data_ptr(), ldb, num_moduli,
+                                   int(bool(fastmode)), work.data_ptr(), computeType, rows[0], rows[1], cols[0],
+                                   cols[1]))
+
+
+def shard_bound(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, work, out_dtype, cols, computeType=REAL_DEFAULT,
+                stream=None):
+    """Accurate mode with sft0 assembled: the bound product over the columns [cols) of op(B)."""
+    _check(lib.gemmul8_shard_bound(_stream(stream), opA, opB, m, n, k, _DTYPE[A.dtype], _DTYPE[B.dtype],
+                                   _DTYPE[out_dtype], A.data_ptr(), lda, B.data_ptr(), ldb, num_moduli,
+                                   work.data_ptr(), computeType, cols[0], cols[1]))
 
 
 def split_bound(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, work, out_dtype, computeType=REAL_DEFAULT,
@@ -159,18 +185,28 @@ def split_bound(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, work, out_dtype, 
     return rowmax, colmax
 
 
-def products(m, n, k, num_moduli, work, mod_begin=0, mod_end=None, computeType=REAL_DEFAULT, stream=None):
-    """Residue planes of moduli [mod_begin, mod_end) (one MFMA launch) into `work`."""
+def products(m, n, k, num_moduli, work, mod_begin=0, mod_end=None, computeType=REAL_DEFAULT, stream=None, cols=None):
+    """Residue planes of moduli [mod_begin, mod_end) (one MFMA launch) into `work`; cols=(c0, c1): those
+    residue columns only (c0 a multiple of 256, c1 one too or n)."""
     mod_end = num_moduli if mod_end is None else mod_end
-    _check(lib.gemmul8_products(_stream(stream), m, n, k, num_moduli, computeType, work.data_ptr(), mod_begin,
-                                mod_end))
+    if cols is None:
+        _check(lib.gemmul8_products(_stream(stream), m, n, k, num_moduli, computeType, work.data_ptr(), mod_begin,
+                                    mod_end))
+    else:
+        _check(lib.gemmul8_products_cols(_stream(stream), m, n, k, num_moduli, computeType, work.data_ptr(),
+                                         mod_begin, mod_end, cols[0], cols[1]))
 
 
-def recombine(m, n, k, num_moduli, alpha, beta, C, ldc, work, computeType=REAL_DEFAULT, stream=None):
-    """CRT of all residue planes in `work` + scaling + alpha/beta epilogue into C."""
+def recombine(m, n, k, num_moduli, alpha, beta, C, ldc, work, computeType=REAL_DEFAULT, stream=None, cols=None):
+    """CRT of all residue planes in `work` + scaling + alpha/beta epilogue into C; cols=(c0, c1): those
+    output columns only, C then holding column c0 first."""
     al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
-    _check(lib.gemmul8_recombine(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], computeType, al.ptr,
-                                 be.ptr, C.data_ptr(), ldc, work.data_ptr()))
+    if cols is None:
+        _check(lib.gemmul8_recombine(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], computeType, al.ptr,
+                                     be.ptr, C.data_ptr(), ldc, work.data_ptr()))
+    else:
+        _check(lib.gemmul8_recombine_cols(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], computeType, al.ptr,
+                                          be.ptr, C.data_ptr(), ldc, work.data_ptr(), cols[0], cols[1]))
 
 
 def residue_planes(work, m, n, k, num_moduli, mod_begin=0, mod_end=None, computeType=REAL_DEFAULT):
@@ -250,6 +286,11 @@ def relerr_dd(C, C1, C2, stream=None):
     cnt = s.numel()
     med = s[cnt // 2] if cnt & 1 else (s[cnt // 2] + s[cnt // 2 - 1]) * 0.5
     return float(s[-1]), float(med)
+
+
+def last_products_kernel():
+    """name of the residue-product kernel the last products launch of this process took"""
+    return lib.gemmul8_last_products_kernel().decode()
 
 
 def mfma_ceiling(iters=4000, stream=None):

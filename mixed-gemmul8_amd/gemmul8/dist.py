@@ -1,35 +1,64 @@
 """gemmul8.dist -- one emulated GEMM sharded over the GPUs of a node.
 
 One process per GPU; torch.distributed with the "nccl" backend (RCCL over xGMI on ROCm).
-The reference has no multi-GPU path; both partitions here return results bit-identical to
-the single-GPU ``gemmul8.gemm`` on the same inputs.
+The reference has no multi-GPU path; its per-modulus loop (GEMMul8/src/gemmul8.cu:259-275: one
+int8 GEMM + one conversion per modulus) is the axis that shards.  Both partitions here return
+results bit-identical to the single-GPU ``gemmul8.gemm`` on the same inputs.
+
+``gemm_moduli`` / ``matmul_moduli``   (the cfg3 partition; strong scaling of ONE product)
+    The work units are (modulus j, column block of C): N * cb units with cb = W / gcd(N, W)
+    column blocks per modulus, N / gcd(N, W) units per rank -- an equal share of the MACs on
+    every rank for any N and W (14 moduli over 8 GPUs: 7 quarter-planes each, where whole
+    planes would give 2,2,2,2,2,2,1,1).  Per call:
+      1. shifts: rank r computes the shifts of its row block of op(A) and its column block of
+         op(B) only (1/W of the stats pass) and the ranks all-gather the int16 vectors
+         (accurate mode: sft0, then the int8 bound product of its column block and one MAX
+         all-reduce of the row / column maxima);
+      2. slices of the moduli its units touch (gemmul8_split, SHIFTS_READY / BOUND_READY);
+      3. the products of its units (gemmul8_products_cols), consecutive units of one modulus in
+         one launch;
+      4. exchange: rank s owns the CRT of the output column block s, so every unit's residue
+         columns go to the owners of those columns.  A column range of a column-major residue
+         plane is one contiguous byte run, sent straight from the workspace into the owner's
+         workspace at the same offset (no packing).  Stage t's transfers are one grouped P2P
+         call posted right after the rank's t-th product launch: RCCL runs them on its own
+         stream behind that launch while the next product runs on the compute stream;
+      5. CRT of its output columns (gemmul8_recombine_cols).
+    C stays distributed by column blocks (``gather=True`` collects it on the root).  Bytes per
+    rank: N * m * n / W residue bytes received (one byte per residue and modulus of its columns,
+    minus what it produced itself) -- at 16384^2, N = 14, W = 8: 0.47 GB per rank, spread over
+    the 7 xGMI links, against 16 B per element per rank (4.3 GB) for reducing partial FP64 CRT
+    sums (which would also reorder the double-double low-word sum) or 3.2 GB into one root for
+    gathering the planes there.
 
 ``matmul_rows``    rank r owns a row block of C = A @ B and computes every modulus for it
-                   from its own rows of A and the full (replicated) B.  The shift of a row of
-                   A depends only on that row and the shifts of B's columns only on B, so the
-                   block equals the matching rows of the single-GPU result.  Nothing crosses
-                   the fabric on the data path in fast mode; the blocks can optionally be
-                   collected on the root (one P2P receive per rank).  Accurate mode derives
-                   B's column shifts from the int8 bound product over ALL rows of A, so the
-                   ranks combine those column maxima (n int32) with one MAX all-reduce before
-                   encoding.  This is the partition bench.py scales.
-``matmul_moduli``  rank r owns the moduli [j0, j1): it computes the shifts (cheap, HBM-bound),
-                   the slices and the residue planes of its moduli only, sending each plane as
-                   soon as its product is launched (the send overlaps the next plane's product),
-                   to the root, which receives every rank's planes concurrently (each sender on
-                   its own xGMI link) into its workspace and runs the CRT over all N planes.
-                   Bytes moved: (N - N_root) * m * n, one byte per residue.  The alternative of
-                   reducing partial FP64 CRT sums would move 16 bytes per element per rank and
-                   reorder the double-double low-word sum, so it is not used.
+    from its own rows of A and the full (replicated) B.  The shift of a row of A depends only
+    on that row and the shifts of B's columns only on B, so the block equals the matching rows
+    of the single-GPU result.  Nothing crosses the fabric on the data path in fast mode.
+    Accurate mode derives B's column shifts from the int8 bound product over ALL rows of A, so
+    the ranks combine those column maxima (n int32) with one MAX all-reduce before encoding.
 
-The compute steps go through an ``ops`` object (default: ``HipOps``, the native library);
-tests substitute a CPU implementation to exercise the communication pattern under gloo.
+The compute steps go through an ``ops`` object (default: the native library); tests substitute
+a CPU implementation to exercise the communication pattern under gloo.  Workspaces are cached per
+shape on the ops object (one object serves one call at a time), so repeated calls allocate only
+their output.
 """
+import math
+
 import torch
 import torch.distributed as dist
 
-from . import (OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, gemm, split, split_bound, products,
-               recombine, residue_planes)
+from . import (OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, gemm, layout, split, split_bound,
+               products, recombine, shard_stats, shard_bound)
+
+TILE = 256  # product tile edge: column blocks of the product units start at multiples of it
+
+
+def blocks(n, parts, align=TILE):
+    """[(b0, b1)] * parts: equal blocks of ceil(n / align / parts) * align, the last ones shorter or empty."""
+    tiles = -(-n // align) if n else 0
+    chunk = -(-tiles // parts) * align if tiles else 0
+    return [(min(i * chunk, n), min((i + 1) * chunk, n)) for i in range(parts)]
 
 
 def moduli_partition(num_moduli, world):
@@ -55,76 +84,321 @@ def row_partition(m, world, align=256):
     return out
 
 
+class ShardPlan:
+    """Who computes what in gemm_moduli (every rank builds the same plan).
+
+    units[r]     rank r's (modulus, c0, c1) product units, in launch order
+    launches[r]  the same with consecutive column blocks of one modulus merged (one launch each)
+    mods[r]      the moduli range [j0, j1) whose slices rank r encodes
+    cols[r]      rank r's output columns (its CRT, and the columns of op(B) whose shifts it computes)
+    rows[r]      the rows of op(A) whose shifts rank r computes
+    """
+
+    def __init__(self, m, n, num_moduli, world, align=TILE):
+        self.m, self.n, self.N, self.world = m, n, num_moduli, world
+        g = math.gcd(num_moduli, world)
+        self.col_blocks = world // g  # column blocks per modulus
+        pcols = blocks(n, self.col_blocks, align)
+        units = [(j, c0, c1) for j in range(num_moduli) for (c0, c1) in pcols]
+        per = len(units) // world  # = N / g
+        self.units = [[u for u in units[r * per:(r + 1) * per] if u[2] > u[1]] for r in range(world)]
+        self.launches = []
+        for us in self.units:
+            merged = []
+            for j, c0, c1 in us:
+                if merged and merged[-1][0] == j and merged[-1][2] == c0:
+                    merged[-1] = (j, merged[-1][1], c1)
+                else:
+                    merged.append((j, c0, c1))
+            self.launches.append(merged)
+        self.mods = [((us[0][0], us[-1][0] + 1) if us else (0, 0)) for us in self.units]
+        self.cols = blocks(n, world, align)
+        self.rows = blocks(m, world, align)
+        self.stages = max((len(x) for x in self.launches), default=0)
+
+    def sends(self, r, t):
+        """[(dst, j, c0, c1)]: residue column runs rank r sends after its launch t"""
+        if t >= len(self.launches[r]):
+            return []
+        j, a, b = self.launches[r][t]
+        out = []
+        for s, (s0, s1) in enumerate(self.cols):
+            lo, hi = max(a, s0), min(b, s1)
+            if s != r and lo < hi:
+                out.append((s, j, lo, hi))
+        return out
+
+    def recvs(self, r, t):
+        """[(src, j, c0, c1)]: residue column runs rank r receives in stage t"""
+        out = []
+        for q in range(self.world):
+            if q != r:
+                out += [(q, j, a, b) for (s, j, a, b) in self.sends(q, t) if s == r]
+        return out
+
+
+# ------------------------------------------------------------------------------------------------
+# native compute steps
+# ------------------------------------------------------------------------------------------------
+class _WorkCache:
+    """workspaces per key, reused across calls (no workspace allocation in a timed loop)"""
+
+    def __init__(self):
+        self._d = {}
+
+    def get(self, key, make):
+        t = self._d.get(key)
+        if t is None:
+            t = self._d[key] = make()
+        return t
+
+    def clear(self):
+        self._d.clear()
+
+
+class HipShardOps:
+    """Native steps of gemm_moduli on the current CUDA (HIP) device and stream."""
+
+    def __init__(self):
+        self.cache = _WorkCache()
+
+    def prepare(self, opA, opB, m, n, k, A, lda, B, ldb, N, fast, out_dtype, ctype):
+        dev = A.device
+        work = self.cache.get(("work", m, n, k, N, ctype, dev), lambda: alloc_work(m, n, k, N, ctype, dev))
+        L = layout(m, n, k, N, ctype)
+        return {"args": (opA, opB, m, n, k, A, lda, B, ldb, N), "fast": fast, "dtype": out_dtype, "ct": ctype,
+                "work": work, "L": L, "m": m, "n": n, "k": k, "N": N, "dev": dev}
+
+    def stats(self, st, rows, cols):
+        opA, opB, m, n, k, A, lda, B, ldb, N = st["args"]
+        shard_stats(opA, opB, m, n, k, A, lda, B, ldb, N, st["fast"], st["work"], st["dtype"], rows, cols, st["ct"])
+
+    def shift_vectors(self, st):
+        """the int16 vectors the ranks assemble: fast sftA [m], sftB [n]; accurate sft0 of A's rows / B's columns"""
+        L, w, m, n = st["L"], st["work"], st["m"], st["n"]
+        if st["fast"]:
+            a, b = L["offSftA"], L["offSftB"]
+        else:
+            a, b = L["offSft0"], L["offSft0"] + 2 * L["bm_pad"]
+        return w[a:a + 2 * m].view(torch.int16), w[b:b + 2 * n].view(torch.int16)
+
+    def bound(self, st, cols):
+        """accurate mode: bound product of the column block -> the int32 maxima area to MAX-combine"""
+        opA, opB, m, n, k, A, lda, B, ldb, N = st["args"]
+        shard_bound(opA, opB, m, n, k, A, lda, B, ldb, N, st["work"], st["dtype"], cols, st["ct"])
+        L = st["L"]
+        o = L["offBound"]
+        return st["work"][o:o + 4 * (L["bm_pad"] + -(-n // TILE) * TILE)].view(torch.int32)
+
+    def encode(self, st, j0, j1):
+        opA, opB, m, n, k, A, lda, B, ldb, N = st["args"]
+        fast = st["fast"]
+        split(opA, opB, m, n, k, A, lda, B, ldb, N, fast, st["work"], st["dtype"], j0, j1, st["ct"],
+              bound_ready=not fast, shifts_ready=fast)
+
+    def products(self, st, j, c0, c1):
+        products(st["m"], st["n"], st["k"], st["N"], st["work"], j, j + 1, st["ct"], cols=(c0, c1))
+
+    def chunks(self, st, j, c0, c1):
+        """uint8 views of the residue columns [c0, c1) of plane j (Karatsuba: one per sub-plane)"""
+        L, w = st["L"], st["work"]
+        base = L["offR"] + j * L["planeR"]
+        subs = [s * L["subR"] for s in range(L["nsub"])]
+        return [w[base + s + c0 * L["ldr"]:base + s + c1 * L["ldr"]] for s in subs]
+
+    def recombine(self, st, c0, c1):
+        m = st["m"]
+        Cb = torch.empty((c1 - c0, m), dtype=st["dtype"], device=st["dev"])
+        if c1 > c0:
+            recombine(m, st["n"], st["k"], st["N"], 1.0, 0.0, Cb, m, st["work"], st["ct"], cols=(c0, c1))
+        return Cb
+
+    def sync(self):
+        torch.cuda.current_stream().synchronize()
+
+
+_default_shard_ops = None
+
+
+def _shard_ops():
+    global _default_shard_ops
+    if _default_shard_ops is None:
+        _default_shard_ops = HipShardOps()
+    return _default_shard_ops
+
+
+def _group_info(group):
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def _global(group, r):
+    return dist.get_global_rank(group, r) if group is not None else r
+
+
+def _allgather_blocks(vec, blks, rank, group):
+    """vec[b0:b1] of every rank's block (blocks(len, W) layout) assembled into every rank's vec"""
+    chunk = blks[0][1] - blks[0][0]
+    if chunk == 0:
+        return
+    b0, b1 = blks[rank]
+    mine = vec.new_zeros(chunk)
+    mine[:b1 - b0] = vec[b0:b1]
+    parts = [vec.new_empty(chunk) for _ in blks]
+    # moved as bytes: RCCL has no 16-bit integer type
+    dist.all_gather([p.view(torch.uint8) for p in parts], mine.view(torch.uint8), group=group)
+    vec.copy_(torch.cat(parts)[:vec.numel()])
+
+
+def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
+                computeType=REAL_DEFAULT, group=None, gather=False, root=0, ops=None, align=TILE, trace=None):
+    """C = op(A) op(B) (column-major operands, alpha = 1, beta = 0) with the work split over the ranks of
+    `group` by (modulus, column block) units; A and B replicated on every rank.
+
+    Returns this rank's output columns [c0, c1) = ShardPlan.cols[rank] as an (c1 - c0, m) tensor (the
+    column-major m x (c1 - c0) block), or with gather=True the whole (n, m) C on the root and None elsewhere.
+    trace: a list that receives (phase, torch.cuda.Event) pairs recorded on the current stream at the phase
+    boundaries (start, shifts, encode, products, exchange, crt)."""
+    ops = ops or _shard_ops()
+    out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
+    rank, world = _group_info(group)
+    plan = ShardPlan(m, n, num_moduli, world, align)  # (align: the native products need TILE)
+    # the gloo backend reads device tensors without waiting on the compute stream
+    host_sync = dist.get_backend(group) != "nccl"
+    st = ops.prepare(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, out_dtype, computeType)
+    c0, c1 = plan.cols[rank]
+
+    def mark(name):
+        if trace is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            trace.append((name, ev))
+
+    mark("start")
+
+    # 1. shifts of this rank's rows / columns, assembled on every rank
+    ops.stats(st, plan.rows[rank], plan.cols[rank])
+    if host_sync:
+        ops.sync()
+    va, vb = ops.shift_vectors(st)
+    _allgather_blocks(va, plan.rows, rank, group)
+    _allgather_blocks(vb, plan.cols, rank, group)
+    if not fastmode:
+        bnd = ops.bound(st, plan.cols[rank])
+        if host_sync:
+            ops.sync()
+        dist.all_reduce(bnd, op=dist.ReduceOp.MAX, group=group)
+    mark("shifts")
+
+    # 2. slices of this rank's moduli
+    j0, j1 = plan.mods[rank]
+    if j1 > j0:
+        ops.encode(st, j0, j1)
+    mark("encode")
+
+    # 3 + 4. products, each launch followed by the grouped transfers of its residue columns
+    reqs = []
+    mine = plan.launches[rank]
+    for t in range(plan.stages):
+        if t < len(mine):
+            ops.products(st, *mine[t])
+        p2p = []
+        for dst, j, a, b in plan.sends(rank, t):
+            p2p += [dist.P2POp(dist.isend, x, _global(group, dst), group) for x in ops.chunks(st, j, a, b)]
+        for src, j, a, b in plan.recvs(rank, t):
+            p2p += [dist.P2POp(dist.irecv, x, _global(group, src), group) for x in ops.chunks(st, j, a, b)]
+        if p2p:
+            if host_sync:
+                ops.sync()
+            reqs += dist.batch_isend_irecv(p2p)
+    mark("products")
+    for q in reqs:
+        q.wait()
+    mark("exchange")
+
+    # 5. CRT of this rank's output columns
+    Cb = ops.recombine(st, c0, c1)
+    mark("crt")
+    if not gather:
+        return Cb
+    if host_sync:
+        ops.sync()
+    if rank != root:
+        if c1 > c0:
+            dist.send(Cb.contiguous(), dst=_global(group, root), group=group)
+        return None
+    C = torch.empty((n, m), dtype=out_dtype, device=Cb.device)
+    C[c0:c1] = Cb
+    rq = [dist.irecv(C[s0:s1], src=_global(group, s), group=group)
+          for s, (s0, s1) in enumerate(plan.cols) if s != root and s1 > s0]
+    for q in rq:
+        q.wait()
+    return C
+
+
+def matmul_moduli(A, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, gather=True, root=0, ops=None,
+                  align=TILE):
+    """C = A @ B (row-major torch tensors, A, B replicated) sharded over the ranks of `group` (gemm_moduli).
+
+    gather=True: the whole C (m x n) on the root, None elsewhere; gather=False: this rank's column block
+    C[:, c0:c1] as an (c1 - c0) x m tensor holding its transpose (the column-major block)."""
+    m, k = A.shape
+    n = B.shape[1]
+    ct = COMPLEX_BIG_MATRIX_ENCODE if A.is_complex() else REAL_DEFAULT
+    # a row-major (m x k) tensor is the column-major k x m matrix: op T on both operands, no copies
+    out = gemm_moduli(OP_T, OP_T, m, n, k, A.contiguous(), k, B.contiguous(), n, num_moduli, fastmode, out_dtype, ct,
+                      group, gather, root, ops, align)
+    return None if out is None else out.t()
+
+
+# ------------------------------------------------------------------------------------------------
+# row partition
+# ------------------------------------------------------------------------------------------------
 class HipOps:
-    """Native compute steps on the current CUDA (HIP) device and stream."""
+    """Native compute steps of matmul_rows on the current CUDA (HIP) device and stream."""
+
+    def __init__(self):
+        self.cache = _WorkCache()
+
+    def _work(self, m, n, k, N, ct, dev):
+        return self.cache.get(("work", m, n, k, N, ct, dev), lambda: alloc_work(m, n, k, N, ct, dev))
 
     def full(self, A, B, num_moduli, fastmode, out_dtype):
         m, k = A.shape
         n = B.shape[1]
         Ct = torch.empty((n, m), dtype=out_dtype, device=A.device)
         if A.is_complex():
-            work = alloc_work(m, n, k, num_moduli, COMPLEX_BIG_MATRIX_ENCODE, A.device)
-            gemm(0, 0, m, n, k, 1.0, A.t().contiguous(), m, B.t().contiguous(), k, 0.0, Ct, m, num_moduli, fastmode,
-                 work, COMPLEX_BIG_MATRIX_ENCODE)
+            ct = COMPLEX_BIG_MATRIX_ENCODE
+            gemm(OP_T, OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, num_moduli, fastmode,
+                 self._work(m, n, k, num_moduli, ct, A.device), ct)
         else:
-            work = alloc_work(m, n, k, num_moduli, REAL_DEFAULT, A.device)
-            gemm(OP_T, OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, num_moduli, fastmode, work)
+            gemm(OP_T, OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, num_moduli, fastmode,
+                 self._work(m, n, k, num_moduli, REAL_DEFAULT, A.device))
         return Ct.t()
 
     def row_bound(self, A, B, num_moduli, out_dtype):
         """Accurate mode: bound product of this row block -> (colmax int32 [n] in the workspace, state)."""
-        if A.is_complex():
-            raise NotImplementedError("accurate mode covers real operands")
         m, k = A.shape
         n = B.shape[1]
-        work = alloc_work(m, n, k, num_moduli, REAL_DEFAULT, A.device)
-        _, colmax = split_bound(OP_T, OP_T, m, n, k, A, k, B, n, num_moduli, work, out_dtype)
-        return colmax, {"A": A, "B": B, "N": num_moduli, "work": work, "dtype": out_dtype}
+        ct = COMPLEX_BIG_MATRIX_ENCODE if A.is_complex() else REAL_DEFAULT
+        work = self._work(m, n, k, num_moduli, ct, A.device)
+        _, colmax = split_bound(OP_T, OP_T, m, n, k, A, k, B, n, num_moduli, work, out_dtype, ct)
+        return colmax, {"A": A, "B": B, "N": num_moduli, "work": work, "dtype": out_dtype, "ct": ct}
 
     def finish_rows(self, st):
-        A, B, N, work = st["A"], st["B"], st["N"], st["work"]
+        A, B, N, work, ct = st["A"], st["B"], st["N"], st["work"], st["ct"]
         m, k = A.shape
         n = B.shape[1]
         Ct = torch.empty((n, m), dtype=st["dtype"], device=A.device)
-        split(OP_T, OP_T, m, n, k, A, k, B, n, N, False, work, st["dtype"], bound_ready=True)
-        products(m, n, k, N, work)
-        recombine(m, n, k, N, 1.0, 0.0, Ct, m, work)
+        split(OP_T, OP_T, m, n, k, A, k, B, n, N, False, work, st["dtype"], computeType=ct, bound_ready=True)
+        products(m, n, k, N, work, computeType=ct)
+        recombine(m, n, k, N, 1.0, 0.0, Ct, m, work, ct)
         return Ct.t()
-
-    def begin(self, A, B, num_moduli, fastmode, out_dtype, j0, j1, need_shifts):
-        """Shifts + slices of moduli [j0, j1) (no products yet) -> state for product() / finish()."""
-        if A.is_complex():
-            raise NotImplementedError("modulus sharding covers real operands")
-        m, k = A.shape
-        n = B.shape[1]
-        work = alloc_work(m, n, k, num_moduli, REAL_DEFAULT, A.device)
-        st = {"m": m, "n": n, "k": k, "N": num_moduli, "work": work, "dtype": out_dtype, "device": A.device}
-        if j1 > j0:
-            split(OP_T, OP_T, m, n, k, A, k, B, n, num_moduli, fastmode, work, out_dtype, j0, j1)
-        elif need_shifts:  # a root that owns no modulus still needs the shifts (one unused slice plane)
-            split(OP_T, OP_T, m, n, k, A, k, B, n, num_moduli, fastmode, work, out_dtype, 0, 1)
-        return st
-
-    def product(self, st, j):
-        """Residue plane j (one launch on the current stream) -> its uint8 [plane] view."""
-        products(st["m"], st["n"], st["k"], st["N"], st["work"], j, j + 1)
-        return residue_planes(st["work"], st["m"], st["n"], st["k"], st["N"], j, j + 1)[0]
-
-    def all_planes(self, st):
-        return residue_planes(st["work"], st["m"], st["n"], st["k"], st["N"])
 
     def sync(self):
         torch.cuda.current_stream().synchronize()
 
-    def finish(self, st):
-        m, n = st["m"], st["n"]
-        Ct = torch.empty((n, m), dtype=st["dtype"], device=st["device"])
-        recombine(m, n, st["k"], st["N"], 1.0, 0.0, Ct, m, st["work"])
-        return Ct.t()
 
-
-def _group_info(group):
-    return dist.get_rank(group), dist.get_world_size(group)
+_default_row_ops = None
 
 
 def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, gather=False, root=0,
@@ -133,7 +407,11 @@ def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=
 
     With gather=True the root returns the full C (rows concatenated in rank order) and the
     other ranks return None."""
-    ops = ops or HipOps()
+    global _default_row_ops
+    if ops is None:
+        if _default_row_ops is None:
+            _default_row_ops = HipOps()
+        ops = _default_row_ops
     out_dtype = out_dtype or torch.promote_types(A_local.dtype, B.dtype)
     rank, world = _group_info(group)
     if fastmode or world == 1:
@@ -150,7 +428,7 @@ def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=
     dist.all_gather(sizes, rows, group=group)
     sizes = [int(s.item()) for s in sizes]
     ops.sync()
-    groot = dist.get_global_rank(group, root) if group is not None else root
+    groot = _global(group, root)
     if rank != root:
         dist.send(C_local.contiguous(), dst=groot, group=group)
         return None
@@ -161,51 +439,8 @@ def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=
             parts.append(C_local)
             continue
         buf = torch.empty((sizes[r], C_local.shape[1]), dtype=C_local.dtype, device=C_local.device)
-        src = dist.get_global_rank(group, r) if group is not None else r
-        reqs.append(dist.irecv(buf, src=src, group=group))
+        reqs.append(dist.irecv(buf, src=_global(group, r), group=group))
         parts.append(buf)
     for q in reqs:
         q.wait()
     return torch.cat(parts, 0)
-
-
-def matmul_moduli(A, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, root=0, ops=None):
-    """C = A @ B with the moduli sharded over the ranks of `group` (A, B replicated).
-
-    Each rank computes its planes one modulus at a time and sends each as soon as it is launched:
-    with RCCL the send of plane j runs on the communication stream behind the products of plane j
-    while the products of plane j + 1 run, and the root receives every rank's planes concurrently
-    (one xGMI link per sender) while computing its own.  Returns C on the root, None elsewhere."""
-    ops = ops or HipOps()
-    out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
-    rank, world = _group_info(group)
-    parts = moduli_partition(num_moduli, world)
-    j0, j1 = parts[rank]
-    # the gloo backend reads device tensors without waiting on the compute stream
-    host_sync = dist.get_backend(group) != "nccl"
-    st = ops.begin(A, B, num_moduli, fastmode, out_dtype, j0, j1, rank == root)
-    groot = dist.get_global_rank(group, root) if group is not None else root
-    if rank != root:
-        reqs = []
-        for j in range(j0, j1):
-            plane = ops.product(st, j)
-            if host_sync:
-                ops.sync()
-            reqs.append(dist.isend(plane, dst=groot, group=group))
-        for q in reqs:
-            q.wait()
-        return None
-    allp = ops.all_planes(st)
-    reqs = []
-    for r in range(world):
-        a, b = parts[r]
-        if r == root:
-            continue
-        src = dist.get_global_rank(group, r) if group is not None else r
-        for j in range(a, b):  # one receive per plane, in the sender's order
-            reqs.append(dist.irecv(allp[j], src=src, group=group))
-    for j in range(j0, j1):
-        ops.product(st, j)
-    for q in reqs:
-        q.wait()
-    return ops.finish(st)

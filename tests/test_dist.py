@@ -50,26 +50,58 @@ class OracleOps:
         C = self.O.crt(self.O.residues(A8, B8), sA, sB, npt)
         return torch.from_numpy(np.ascontiguousarray(C))
 
-    def begin(self, A, B, N, fast, out_dtype, j0, j1, need_shifts):
-        A8, B8, sA, sB = self.O.scaling(A.numpy(), B.numpy(), N, fast)
-        full = self.O.residues(A8, B8)
-        Rt = torch.zeros((N, full[0].size), dtype=torch.uint8)  # planes arrive one by one
-        npt = torch.empty((), dtype=out_dtype).numpy().dtype
-        return {"R": Rt, "full": full, "shape": full.shape, "sA": sA, "sB": sB, "dtype": npt}
-
-    def product(self, st, j):
-        st["R"][j] = torch.from_numpy(st["full"][j].reshape(-1))
-        return st["R"][j]
-
-    def all_planes(self, st):
-        return st["R"]
-
     def sync(self):
         pass
 
-    def finish(self, st):
-        C = self.O.crt(st["R"].numpy().reshape(st["shape"]), st["sA"], st["sB"], st["dtype"])
-        return torch.from_numpy(np.ascontiguousarray(C))
+
+class OracleShardOps:
+    """CPU stand-in for gemmul8.dist.HipShardOps (tests only).  The shifts and residues are computed
+    in full by the oracle but published only for this rank's rows / columns / units, so the result
+    is right only if gemm_moduli's all-gathers and residue exchange deliver every other part."""
+
+    SENTINEL = -32768
+
+    def __init__(self):
+        from oracle import oracle as O
+        self.O = O
+
+    def prepare(self, opA, opB, m, n, k, A, lda, B, ldb, N, fast, out_dtype, ct):
+        # column-major operands: an (x, ld) row-major tensor holds the column-major ld x x matrix
+        Acm = A.numpy().T[:lda]
+        Bcm = B.numpy().T[:ldb]
+        A8, B8, sA, sB = self.O.scaling(Acm, Bcm, N, fast, opA=opA, opB=opB)
+        full = self.O.residues(A8, B8)
+        npt = torch.empty((), dtype=out_dtype).numpy().dtype
+        return {"sA": sA, "sB": sB, "full": full, "R": torch.zeros(full.shape, dtype=torch.uint8),
+                "pA": torch.full((m,), self.SENTINEL, dtype=torch.int16),
+                "pB": torch.full((n,), self.SENTINEL, dtype=torch.int16), "dtype": npt}
+
+    def stats(self, st, rows, cols):
+        st["pA"][rows[0]:rows[1]] = torch.from_numpy(st["sA"][rows[0]:rows[1]])
+        st["pB"][cols[0]:cols[1]] = torch.from_numpy(st["sB"][cols[0]:cols[1]])
+
+    def shift_vectors(self, st):
+        return st["pA"], st["pB"]
+
+    def bound(self, st, cols):
+        return torch.zeros(8, dtype=torch.int32)  # (the oracle derives accurate shifts itself)
+
+    def encode(self, st, j0, j1):
+        pass
+
+    def products(self, st, j, c0, c1):
+        st["R"][j, c0:c1] = torch.from_numpy(st["full"][j, c0:c1])
+
+    def chunks(self, st, j, c0, c1):
+        return [st["R"][j, c0:c1].view(-1)]
+
+    def recombine(self, st, c0, c1):
+        C = self.O.crt(np.ascontiguousarray(st["R"][:, c0:c1].numpy()), st["pA"].numpy(),
+                       np.ascontiguousarray(st["pB"][c0:c1].numpy()), st["dtype"])
+        return torch.from_numpy(np.ascontiguousarray(C.T))
+
+    def sync(self):
+        pass
 
 
 def _worker(rank, world, port, case, outdir):
@@ -82,11 +114,16 @@ def _worker(rank, world, port, case, outdir):
         A = ((rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))).astype(dt)
         B = ((rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))).astype(dt)
         ops = OracleOps()
-        Cm = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, ops=ops)
+        # small column blocks (align 16) so that every rank owns units and output columns
+        Cm = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, ops=OracleShardOps(), align=16)
+        # the column block of this rank without the gather (C stays distributed)
+        Cb = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, gather=False, ops=OracleShardOps(),
+                              align=16)
+        np.save(os.path.join(outdir, f"block{rank}.npy"), Cb.contiguous().numpy())
         r0, r1 = GD.row_partition(m, world, align=16)[rank]
         Cr = GD.matmul_rows(torch.from_numpy(A[r0:r1].copy()), torch.from_numpy(B), N, fast, gather=True, ops=ops)
         if rank == 0:
-            np.save(os.path.join(outdir, "moduli.npy"), Cm.numpy())
+            np.save(os.path.join(outdir, "moduli.npy"), Cm.contiguous().numpy())
             np.save(os.path.join(outdir, "rows.npy"), Cr.numpy())
         else:
             assert Cm is None and Cr is None
@@ -101,6 +138,8 @@ def _worker(rank, world, port, case, outdir):
     (3, (100, 40, 64, 14, True, np.float64)),
     (3, (48, 30, 50, 8, True, np.float32)),
     (3, (90, 30, 70, 9, False, np.float64)),
+    (4, (100, 70, 64, 14, True, np.float64)),
+    (2, (40, 50, 60, 6, True, np.complex128)),
 ])
 def test_sharded_equals_single_call(tmp_path, world, case):
     sys.path.insert(0, ROOT)
@@ -115,6 +154,11 @@ def test_sharded_equals_single_call(tmp_path, world, case):
         got = np.load(tmp_path / f"{name}.npy")
         assert got.shape == C.shape
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C).view(np.uint8)), name
+    from gemmul8.dist import ShardPlan
+    for r, (c0, c1) in enumerate(ShardPlan(m, n, N, world, 16).cols):
+        got = np.load(tmp_path / f"block{r}.npy")
+        assert got.shape == (m, c1 - c0)
+        assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C[:, c0:c1]).view(np.uint8)), r
 
 
 def test_partitions():

@@ -19,8 +19,12 @@ pytestmark = pytest.mark.gpu
 def _rand(m, n, seed, dtype):
     import torch
     g = torch.Generator().manual_seed(seed)
-    x = (torch.rand((m, n), generator=g, dtype=torch.float64) - 0.5) * torch.exp(
-        torch.randn((m, n), generator=g, dtype=torch.float64))
+    def one():
+        return (torch.rand((m, n), generator=g, dtype=torch.float64) - 0.5) * torch.exp(
+            torch.randn((m, n), generator=g, dtype=torch.float64))
+    x = one()
+    if dtype.is_complex:
+        x = torch.complex(x, one())
     return x.to(dtype).cuda()
 
 
@@ -30,8 +34,9 @@ def _single(A, B, N, fast, out_dtype):
     m, k = A.shape
     n = B.shape[1]
     Ct = torch.empty((n, m), dtype=out_dtype, device="cuda")
-    work = G.alloc_work(m, n, k, N)
-    G.gemm(G.OP_T, G.OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, N, fast, work)
+    ct = G.COMPLEX_BIG_MATRIX_ENCODE if A.is_complex() else G.REAL_DEFAULT
+    work = G.alloc_work(m, n, k, N, ct)
+    G.gemm(G.OP_T, G.OP_T, m, n, k, 1.0, A, k, B, n, 0.0, Ct, m, N, fast, work, ct)
     torch.cuda.synchronize()
     return Ct.t().contiguous()
 
@@ -100,23 +105,23 @@ def test_accurate_row_blocks_with_combined_bound():
     m, n, k, N = 700, 300, 400, 12
     A, B = _rand(m, k, 3, torch.float64), _rand(k, n, 4, torch.float64)
     ref = _single(A, B, N, False, torch.float64)
-    ops = GD.HipOps()
     blocks = GD.row_partition(m, 3)
+    ops = [GD.HipOps() for _ in blocks]  # one per simulated rank (each caches its own workspace)
     states, colmaxes = [], []
-    for r0, r1 in blocks:
-        cm, st = ops.row_bound(A[r0:r1].contiguous(), B, N, torch.float64)
+    for (r0, r1), o in zip(blocks, ops):
+        cm, st = o.row_bound(A[r0:r1].contiguous(), B, N, torch.float64)
         colmaxes.append(cm)
         states.append(st)
     torch.cuda.synchronize()
     comb = torch.stack([c.clone() for c in colmaxes]).amax(0)
     for c in colmaxes:  # what the MAX all-reduce leaves in every rank's workspace
         c.copy_(comb)
-    out = torch.cat([ops.finish_rows(st) for st in states], 0)
+    out = torch.cat([o.finish_rows(st) for o, st in zip(ops, states)], 0)
     torch.cuda.synchronize()
     assert _same(out, ref)
     # without the exchange the column shifts differ (the reason the all-reduce exists)
-    cm, st = ops.row_bound(A[:256].contiguous(), B, N, torch.float64)
-    alone = ops.finish_rows(st)
+    cm, st = ops[0].row_bound(A[:256].contiguous(), B, N, torch.float64)
+    alone = ops[0].finish_rows(st)
     torch.cuda.synchronize()
     assert not _same(alone, ref[:256])
 
@@ -141,6 +146,7 @@ def test_dist_one_rank_rccl():
         A, B = _rand(m, k, 5, torch.float64), _rand(k, n, 6, torch.float64)
         ref = _single(A, B, N, True, torch.float64)
         assert _same(GD.matmul_moduli(A, B, N, True), ref)
+        assert _same(GD.matmul_moduli(A, B, N, True, gather=False), ref)
         assert _same(GD.matmul_rows(A, B, N, True, gather=True), ref)
         refa = _single(A, B, N, False, torch.float64)
         assert _same(GD.matmul_rows(A, B, N, False), refa)
@@ -149,27 +155,107 @@ def test_dist_one_rank_rccl():
         dist.destroy_process_group()
 
 
-def test_moduli_shards_assembled_on_root():
-    """The modulus-sharded data flow of matmul_moduli with 4 simulated ranks in one process:
-    each 'rank' fills its own workspace, the root copies the planes in (the P2P receive)."""
+def _simulate_moduli_shards(opA, opB, m, n, k, A, lda, B, ldb, N, fast, out_dtype, ct, world, align=256):
+    """gemm_moduli's data flow with `world` simulated ranks in one process, each with its own workspace
+    (HipShardOps instance): shift blocks assembled, bound maxima MAX-combined, residue column runs copied
+    from the producing rank's workspace into the owner's (the P2P transfers), per-rank CRT of its columns."""
     import torch
     from gemmul8 import dist as GD
-    m, n, k, N = 384, 256, 300, 14
-    A, B = _rand(m, k, 7, torch.float64), _rand(k, n, 8, torch.float64)
-    ref = _single(A, B, N, True, torch.float64)
-    ops = GD.HipOps()
-    parts = GD.moduli_partition(N, 4)
-    states = [ops.begin(A, B, N, True, torch.float64, a, b, r == 0) for r, (a, b) in enumerate(parts)]
-    root_st = states[0]
-    allp = ops.all_planes(root_st)
-    for r, (a, b) in enumerate(parts):
-        for j in range(a, b):  # plane by plane, as matmul_moduli sends them
-            plane = ops.product(states[r], j)
-            if r:
-                allp[j].copy_(plane)
-    out = ops.finish(root_st)
+    plan = GD.ShardPlan(m, n, N, world, align)
+    ops = [GD.HipShardOps() for _ in range(world)]
+    st = [o.prepare(opA, opB, m, n, k, A, lda, B, ldb, N, fast, out_dtype, ct) for o in ops]
+    for r in range(world):
+        ops[r].stats(st[r], plan.rows[r], plan.cols[r])
+    vecs = [ops[r].shift_vectors(st[r]) for r in range(world)]
+    for r in range(world):  # the all-gathers
+        (a0, a1), (b0, b1) = plan.rows[r], plan.cols[r]
+        for q in range(world):
+            if q != r:
+                vecs[q][0][a0:a1] = vecs[r][0][a0:a1]
+                vecs[q][1][b0:b1] = vecs[r][1][b0:b1]
+    if not fast:
+        bnd = [ops[r].bound(st[r], plan.cols[r]).clone() for r in range(world)]
+        comb = torch.stack(bnd).amax(0)
+        for r in range(world):  # the MAX all-reduce
+            L = st[r]["L"]
+            st[r]["work"][L["offBound"]:L["offBound"] + 4 * comb.numel()].view(torch.int32).copy_(comb)
+    for r in range(world):
+        j0, j1 = plan.mods[r]
+        if j1 > j0:
+            ops[r].encode(st[r], j0, j1)
+    for t in range(plan.stages):
+        for r in range(world):
+            if t < len(plan.launches[r]):
+                ops[r].products(st[r], *plan.launches[r][t])
+        for r in range(world):
+            for dst, j, a, b in plan.sends(r, t):
+                for x, y in zip(ops[r].chunks(st[r], j, a, b), ops[dst].chunks(st[dst], j, a, b)):
+                    y.copy_(x)
+    out = [ops[r].recombine(st[r], *plan.cols[r]).clone() for r in range(world)]
     torch.cuda.synchronize()
-    assert _same(out, ref)
+    return torch.cat(out, 0), plan
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("m,n,k,N,fast,dt", [
+    (600, 1500, 500, 14, True, "f64"),
+    (520, 1300, 333, 9, False, "f64"),
+    (300, 1100, 256, 6, True, "f32"),
+    (700, 1025, 300, 12, True, "c128"),
+    (300, 900, 200, 10, False, "c128"),
+])
+def test_moduli_column_shards_simulated(world, m, n, k, N, fast, dt):
+    """the (modulus, column block) partition of gemm_moduli through the native sharded entry points
+    (gemmul8_shard_stats / _shard_bound / _split SHIFTS_READY / _products_cols / _recombine_cols),
+    simulated ranks in one process: bit-identical to one gemm call"""
+    import torch
+    import gemmul8 as G
+    tdt = {"f64": torch.float64, "f32": torch.float32, "c128": torch.complex128}[dt]
+    ct = G.COMPLEX_BIG_MATRIX_ENCODE if tdt.is_complex else G.REAL_DEFAULT
+    A, B = _rand(m, k, 21, tdt), _rand(k, n, 22, tdt)  # row-major = column-major transposes: op T
+    ref = torch.empty((n, m), dtype=tdt, device="cuda")
+    G.gemm(G.OP_T, G.OP_T, m, n, k, 1.0, A, k, B, n, 0.0, ref, m, N, fast, G.alloc_work(m, n, k, N, ct), ct)
+    got, plan = _simulate_moduli_shards(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, fast, tdt, ct, world)
+    for j in range(N):  # every modulus' columns covered exactly once
+        assert sum(c1 - c0 for us in plan.units for (jj, c0, c1) in us if jj == j) == n
+    assert _same(got, ref)
+
+
+def test_moduli_column_shards_karatsuba_and_op_n():
+    """complex at a Karatsuba shape (k >= 3072, m >= 1024: 3 residue sub-planes, one column run per
+    sub-plane) and column-major op N operands, fast and accurate"""
+    import torch
+    import gemmul8 as G
+    m, n, k, N = 1024, 800, 3100, 12
+    ct = G.COMPLEX_BIG_MATRIX_ENCODE
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn((k, m), dtype=torch.complex128, device="cuda", generator=g)  # column-major m x k
+    B = torch.randn((n, k), dtype=torch.complex128, device="cuda", generator=g)  # column-major k x n
+    for fast in (True, False):
+        ref = torch.empty((n, m), dtype=torch.complex128, device="cuda")
+        G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, ref, m, N, fast, G.alloc_work(m, n, k, N, ct), ct)
+        got, _ = _simulate_moduli_shards(0, 0, m, n, k, A, m, B, k, N, fast, torch.complex128, ct, 4)
+        assert _same(got, ref), fast
+
+
+def test_products_cols_and_recombine_cols_compose():
+    """products over column ranges + CRT over column ranges == one call (one workspace)"""
+    import torch
+    import gemmul8 as G
+    m, n, k, N = 500, 1000, 700, 14
+    A, B = _rand(m, k, 31, torch.float64), _rand(k, n, 32, torch.float64)
+    ref = _single(A, B, N, True, torch.float64)
+    work = G.alloc_work(m, n, k, N)
+    G.split(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, work, torch.float64)
+    for j0, j1, c0, c1 in ((0, 5, 0, 256), (0, 5, 256, 1000), (5, 14, 0, 768), (5, 14, 768, 1000)):
+        G.products(m, n, k, N, work, j0, j1, cols=(c0, c1))
+    Ct = torch.empty((n, m), dtype=torch.float64, device="cuda")
+    for c0, c1 in ((0, 300), (300, 301), (301, 1000)):
+        G.recombine(m, n, k, N, 1.0, 0.0, Ct[c0:c1], m, work, cols=(c0, c1))
+    torch.cuda.synchronize()
+    assert _same(Ct.t(), ref)
+    with pytest.raises(G.Gemmul8Error):
+        G.products(m, n, k, N, work, 0, 1, cols=(100, 300))  # column ranges start on a tile
 
 
 @pytest.mark.parametrize("S", [1, 3, 13])
@@ -217,18 +303,22 @@ rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 torch.cuda.set_device(0)  # the ranks share the one GPU; gloo carries the messages
 dist.init_process_group("gloo")
 try:
-    m, n, k, N = 700, 300, 400, 14
-    A, B = _rand(m, k, 11, torch.float64), _rand(k, n, 12, torch.float64)
+    m, n, k, N = 700, 1100, 400, 14
     ok = True
-    for fast in (True, False):
-        ref = _single(A, B, N, fast, torch.float64) if rank == 0 else None
-        C = GD.matmul_moduli(A, B, N, fast)
-        if rank == 0:
-            ok &= _same(C, ref)
-        r0, r1 = GD.row_partition(m, world)[rank]
-        Cr = GD.matmul_rows(A[r0:r1].contiguous(), B, N, fast, gather=True)
-        if rank == 0:
-            ok &= _same(Cr, ref)
+    for dt in (torch.float64, torch.complex128):
+        A, B = _rand(m, k, 11, dt), _rand(k, n, 12, dt)
+        for fast in (True, False):
+            ref = _single(A, B, N, fast, dt)
+            C = GD.matmul_moduli(A, B, N, fast)
+            if rank == 0:
+                ok &= _same(C, ref)
+            Cb = GD.matmul_moduli(A, B, N, fast, gather=False)
+            c0, c1 = GD.ShardPlan(m, n, N, world).cols[rank]
+            ok &= _same(Cb, ref[:, c0:c1])
+            r0, r1 = GD.row_partition(m, world)[rank]
+            Cr = GD.matmul_rows(A[r0:r1].contiguous(), B, N, fast, gather=True)
+            if rank == 0:
+                ok &= _same(Cr, ref)
     dist.barrier()
     if rank == 0:
         print("RESULT", "OK" if ok else "MISMATCH")
@@ -238,9 +328,10 @@ finally:
 
 
 def test_dist_three_ranks_on_one_gpu_gloo():
-    """gemmul8.dist with three processes on the one GPU (gloo messages): the modulus partition with
-    its per-plane sends and the row partition (accurate mode: the MAX all-reduce of the column
-    bounds) on the native kernels, bit-identical to the single call"""
+    """gemmul8.dist with three processes on the one GPU (gloo messages): the (modulus, column block)
+    partition with its shift all-gathers, bound all-reduce and staged residue exchange, gathered
+    and distributed, and the row partition (accurate mode: the MAX all-reduce of the column bounds),
+    real and complex, on the native kernels, bit-identical to the single call"""
     import subprocess
     import sys
     tdir = os.path.dirname(os.path.abspath(__file__))
