@@ -170,7 +170,7 @@ def cpu_baseline(size_hint, dev):
     cfg1 = {"workload": "cfg1: SGEMM emulation m=n=k=1024, num_moduli=4, fast mode (CPU, full size)",
             "seconds": round(dt1, 3), "tflops": 2.0 * 1024 ** 3 / dt1 / 1e12, "threads": threads,
             "relerr_max_vs_fp64": float(rel1.max()), "relerr_median_vs_fp64": float(np.median(rel1)),
-            "sha256_C": hashlib.sha256(np.asfortranarray(C1).tobytes()).hexdigest()}
+            "sha256_C": hashlib.sha256(np.asfortranarray(C1).tobytes(order="F")).hexdigest()}
     fx = os.path.join(ROOT, "tests", "golden", "cfg1_ref.json")
     if os.path.exists(fx):
         ref1 = json.load(open(fx))

@@ -13,7 +13,8 @@
  * Return codes: 0 ok, GEMMUL8_E_* < 0 on invalid arguments (nothing enqueued).
  * GEMMUL8_E_HIP: a kernel launch of THIS call failed; the phases after it were not enqueued
  * (C is written only by the last phase).  An error left pending on the calling thread by
- * earlier HIP calls is cleared at entry, not reported as the call's own.
+ * earlier HIP calls is neither reported as the call's own nor cleared (hipGetLastError still
+ * returns it to the application).
  */
 #ifndef GEMMUL8_C_H
 #define GEMMUL8_C_H

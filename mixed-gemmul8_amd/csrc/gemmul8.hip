@@ -208,12 +208,12 @@ struct Phase {
 };
 }  // namespace timing
 
-// Launch errors: every entry point that enqueues work first clears an error left pending on the
-// calling thread by earlier, unrelated HIP calls (hipGetLastError would otherwise report it as
-// ours), then checks after each phase, so GEMMUL8_E_HIP always means a launch of THIS call failed
-// and no later phase was enqueued.
-static inline void clear_stale_error() { (void)hipGetLastError(); }
-static inline bool launch_ok() { return hipGetLastError() == hipSuccess; }
+// Launch errors: every library launch checks its own return code (launch(), oz2_split.hpp); an entry
+// point resets the thread's failure flag first and checks it after each phase, so GEMMUL8_E_HIP always
+// means a launch of THIS call failed and no later phase was enqueued.  An error the application left
+// pending on the thread (hipGetLastError) is neither reported as ours nor cleared.
+static inline void clear_stale_error() { g_launch_failed = false; }
+static inline bool launch_ok() { return !g_launch_failed; }
 static bool is_capturing(hipStream_t st) {
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     return hipStreamIsCapturing(st, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone;
@@ -734,7 +734,7 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
     oz2::clear_stale_error();
     oz2::gemm_i8(base + L.offA, base + L.offB, L, 1, oz2::Epi::RAW, C32, nullptr, nullptr, MP,
                  static_cast<hipStream_t>(stream));
-    return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
 
 const char *gemmul8_last_products_kernel(void) {

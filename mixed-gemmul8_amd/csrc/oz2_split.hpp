@@ -3,6 +3,7 @@
 #include <hip/hip_ext.h>
 
 #include <atomic>
+#include <tuple>
 
 #include "oz2_common.hpp"
 
@@ -23,16 +24,30 @@ struct PhaseEvents {
     bool stop_taken;
 };
 inline thread_local PhaseEvents g_phase_ev{};
+// a library launch on this thread failed since the entry point began (set from the launch's own return
+// code, so an error the application left pending on the thread is neither reported nor consumed)
+inline thread_local bool g_launch_failed = false;
 
 template <typename... KArgs, typename... Args>
 inline void launch(void (*kernel)(KArgs...), dim3 grid, dim3 block, hipStream_t st, Args... args) {
+    std::tuple<KArgs...> kargs(static_cast<KArgs>(args)...);
+    void *ptrs[sizeof...(KArgs) > 0 ? sizeof...(KArgs) : 1] = {};
+    std::apply([&](auto &...x) {
+        int i = 0;
+        ((ptrs[i++] = const_cast<void *>(static_cast<const void *>(&x))), ...);
+    }, kargs);
     PhaseEvents &e = g_phase_ev;
+    hipError_t rc;
     if (e.st == st && (e.start || e.stop)) {
-        hipExtLaunchKernelGGL(kernel, grid, block, 0, st, e.start, e.stop, 0, args...);
+        rc = hipExtLaunchKernel(reinterpret_cast<const void *>(kernel), grid, block, ptrs, 0, st, e.start, e.stop, 0);
         e.start = nullptr;
         e.stop_taken = e.stop != nullptr;
     } else {
-        hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+        rc = hipLaunchKernel(reinterpret_cast<const void *>(kernel), grid, block, ptrs, 0, st);
+    }
+    if (rc != hipSuccess) {
+        g_launch_failed = true;
+        (void)hipGetLastError();  // our own failure, reported through the return code instead
     }
 }
 

@@ -165,6 +165,8 @@ rc = hip.hipSetDevice(ctypes.c_int(12345))     # fails: leaves hipErrorInvalidDe
 out["stale_set"] = bool(rc != 0 and hip.hipPeekAtLastError() != 0)
 try:
     C5.addmm_(A5, B5, beta=0.5)                  # -> hipblasDgemm with beta = 0.5
+    out["stale_still_pending"] = bool(hip.hipPeekAtLastError() != 0)  # not consumed by the emulator
+    hip.hipGetLastError()
     torch.cuda.synchronize()
     out["stale_beta_bits"] = bool(torch.equal(C5, Cexp))
 except RuntimeError as e:                        # torch itself reported the pending error first
