@@ -14,7 +14,9 @@
 //                                 default fp64_int8_14 (fast mode)
 //   GEMMUL8_COMPUTE_MODE_SGEMM    S and C GEMM: "sgemm" (forward, default) or "fp32_int8_<N>[_accu]"
 //   GEMMUL8_COMPLEX_TYPE          big_matrix (default) | classic | karatsuba
-//   GEMMUL8_INTERCEPT_THRESHOLD_M / _N / _K   emulate only when m, n, k are all >= (default 128)
+//   GEMMUL8_INTERCEPT_THRESHOLD_M / _N / _K   emulate only when m, n, k are all >= (default 1536: the
+//                                 measured square crossover on MI355X, below which rocBLAS DGEMM is as fast
+//                                 or faster -- INTEGRATION.md section 3)
 //   GEMMUL8_INFO=1                one line per call on stderr
 // Calls with device-resident alpha/beta (pointer mode device), sizes below the thresholds or
 // arguments the emulator rejects (nothing enqueued) go to the vendor routine unchanged.  The Ex forms
@@ -154,7 +156,8 @@ Mode parse_mode(const char *name, const char *prefix, bool default_on) {
 struct Config {
     Mode d, s;
     int ctype = GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE;
-    long tm = 128, tn = 128, tk = 128;
+    static constexpr long DEFAULT_THRESHOLD = 1536;
+    long tm = DEFAULT_THRESHOLD, tn = DEFAULT_THRESHOLD, tk = DEFAULT_THRESHOLD;
     bool info = false;
     Config() {
         d = parse_mode("GEMMUL8_COMPUTE_MODE", "fp64_int8_", true);
@@ -167,9 +170,9 @@ struct Config {
             const char *v = getenv(e);
             return v && *v ? strtol(v, nullptr, 10) : dflt;
         };
-        tm = num("GEMMUL8_INTERCEPT_THRESHOLD_M", 128);
-        tn = num("GEMMUL8_INTERCEPT_THRESHOLD_N", 128);
-        tk = num("GEMMUL8_INTERCEPT_THRESHOLD_K", 128);
+        tm = num("GEMMUL8_INTERCEPT_THRESHOLD_M", DEFAULT_THRESHOLD);
+        tn = num("GEMMUL8_INTERCEPT_THRESHOLD_N", DEFAULT_THRESHOLD);
+        tk = num("GEMMUL8_INTERCEPT_THRESHOLD_K", DEFAULT_THRESHOLD);
         info = num("GEMMUL8_INFO", 0) != 0;
     }
 };

@@ -20,6 +20,9 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIJACK = os.path.join(ROOT, "mixed-gemmul8_amd", "gemmul8", "libgemmul8_hijack.so")
+# the tests below run small shapes: the interposer's default thresholds (1536) would forward them
+SMALL_THRESHOLDS = {"GEMMUL8_INTERCEPT_THRESHOLD_M": "128", "GEMMUL8_INTERCEPT_THRESHOLD_N": "128",
+                    "GEMMUL8_INTERCEPT_THRESHOLD_K": "128"}
 
 CHILD = r'''
 import ctypes, json, os, sys
@@ -265,7 +268,7 @@ print("RESULT " + json.dumps(out))
 
 def test_ex_and_batched_forms():
     assert os.path.exists(HIJACK), "libgemmul8_hijack.so not built"
-    env = dict(os.environ, GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14")
+    env = dict(os.environ, GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14", **SMALL_THRESHOLDS)
     r = subprocess.run([sys.executable, "-c", CHILD_EX, HIJACK, os.path.join(ROOT, "mixed-gemmul8_amd")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -290,7 +293,7 @@ def test_ex_and_batched_forms():
 
 def test_torch_matmul_is_emulated():
     assert os.path.exists(HIJACK), "libgemmul8_hijack.so not built"
-    env = dict(os.environ, GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14")
+    env = dict(os.environ, GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14", **SMALL_THRESHOLDS)
     r = subprocess.run([sys.executable, "-c", CHILD, HIJACK, os.path.join(ROOT, "mixed-gemmul8_amd")], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -316,3 +319,37 @@ def test_torch_matmul_is_emulated():
     assert res["stale_set"], res
     assert res.get("stale_beta_bits"), res
     assert "launch failed" not in log, log[-2000:]
+
+
+CHILD_DEFAULT = r'''
+import ctypes, json, os, sys
+hj = ctypes.CDLL(sys.argv[1], mode=ctypes.RTLD_GLOBAL)
+import torch
+sys.path.insert(0, sys.argv[2])
+import gemmul8 as G
+g = torch.Generator(device="cuda").manual_seed(3)
+out = {}
+for s in (512, 1024, 2048):
+    A = torch.randn(s, s, dtype=torch.float64, device="cuda", generator=g)
+    B = torch.randn(s, s, dtype=torch.float64, device="cuda", generator=g)
+    C = torch.matmul(A, B)
+    E = G.matmul(B.t().contiguous(), A.t().contiguous(), 14).t()
+    out[str(s)] = bool(torch.equal(C, E))
+print("RESULT " + json.dumps(out))
+'''
+
+
+def test_default_thresholds_follow_the_crossover():
+    """with no threshold set, DGEMMs below the measured MI355X crossover (1536) keep the vendor routine
+    (512^3, 1024^3) and larger ones are emulated (2048^3, bit for bit)"""
+    assert os.path.exists(HIJACK), "libgemmul8_hijack.so not built"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("GEMMUL8_INTERCEPT_THRESHOLD")}
+    env.update(GEMMUL8_INFO="1", GEMMUL8_COMPUTE_MODE="fp64_int8_14")
+    r = subprocess.run([sys.executable, "-c", CHILD_DEFAULT, HIJACK, os.path.join(ROOT, "mixed-gemmul8_amd")],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")][-1][len("RESULT "):])
+    log = r.stderr
+    assert "m=2048 n=2048 k=2048 -> emulated" in log, log[-2000:]
+    assert "m=512 " not in log and "m=1024 " not in log, log[-2000:]
+    assert res["2048"] and not res["512"], res
