@@ -265,15 +265,15 @@ def main():
     fmac = (3.0 if G.layout(m, n, k, N, ct)["nsub"] == 3 else 4.0) if cplx else 1.0
     if sharded:
         # dominant kernel: the int8 products of rank 0's units (one products_cols launch per merged unit)
-        ops_step = sum(2.0 * m * (c1 - c0) * k * fmac for _, c0, c1 in plan.launches[rank])
-        planes = sum(c1 - c0 for _, c0, c1 in plan.launches[rank]) / n
+        ops_step = sum(2.0 * m * (c1 - c0) * k * fmac * (j1 - j0) for j0, j1, c0, c1 in plan.launches[rank])
+        planes = sum((c1 - c0) * (j1 - j0) for j0, j1, c0, c1 in plan.launches[rank]) / n
         seg = {}
         for i in range(0, len(trace), 6):
             evs = trace[i:i + 6]
             for (a, ea), (b, eb) in zip(evs, evs[1:]):
                 seg[b] = seg.get(b, 0.0) + ea.elapsed_time(eb)
         extra["step_phases_ms_rank0"] = {kk: round(v / args.steps, 4) for kk, v in seg.items()}
-        extra["units_rank0"] = [list(u) for u in plan.launches[rank]]
+        extra["launches_rank0"] = [list(u) for u in plan.launches[rank]]
     else:
         ops_step = 2.0 * fmac * m * n * k * N
         planes = N

@@ -15,14 +15,15 @@ results bit-identical to the single-GPU ``gemmul8.gemm`` on the same inputs.
          (accurate mode: sft0, then the int8 bound product of its column block and one MAX
          all-reduce of the row / column maxima);
       2. slices of the moduli its units touch (gemmul8_split, SHIFTS_READY / BOUND_READY);
-      3. the products of its units (gemmul8_products_cols), consecutive units of one modulus in
-         one launch;
+      3. the products of its units (gemmul8_products_cols), cut at the output-column owners'
+         boundaries: first the pieces other ranks own, then its own (ShardPlan._schedule);
       4. exchange: rank s owns the CRT of the output column block s, so every unit's residue
          columns go to the owners of those columns.  A column range of a column-major residue
          plane is one contiguous byte run, sent straight from the workspace into the owner's
          workspace at the same offset (no packing).  Stage t's transfers are one grouped P2P
          call posted right after the rank's t-th product launch: RCCL runs them on its own
-         stream behind that launch while the next product runs on the compute stream;
+         stream behind that launch while the next product runs on the compute stream, and the
+         last launches (the rank's own columns) send nothing, so the final transfers overlap them;
       5. CRT of its output columns (gemmul8_recombine_cols).
     C stays distributed by column blocks (``gather=True`` collects it on the root).  Bytes per
     rank: N * m * n / W residue bytes received (one byte per residue and modulus of its columns,
@@ -87,11 +88,15 @@ def row_partition(m, world, align=256):
 class ShardPlan:
     """Who computes what in gemm_moduli (every rank builds the same plan).
 
-    units[r]     rank r's (modulus, c0, c1) product units, in launch order
-    launches[r]  the same with consecutive column blocks of one modulus merged (one launch each)
-    mods[r]      the moduli range [j0, j1) whose slices rank r encodes
+    units[r]     rank r's (modulus, c0, c1) product units
     cols[r]      rank r's output columns (its CRT, and the columns of op(B) whose shifts it computes)
     rows[r]      the rows of op(A) whose shifts rank r computes
+    launches[r]  rank r's product launches (j0, j1, c0, c1): its units cut at the output-column owners'
+                 boundaries; the pieces other ranks own first (consecutive columns of one modulus merged
+                 into one launch, each launch's transfers posted right behind it), then the pieces it owns
+                 itself (one launch over several moduli where they share the columns), which need no
+                 transfer -- so the last transfers run under those products instead of after them
+    mods[r]      the moduli range [j0, j1) whose slices rank r encodes
     """
 
     def __init__(self, m, n, num_moduli, world, align=TILE):
@@ -102,31 +107,38 @@ class ShardPlan:
         units = [(j, c0, c1) for j in range(num_moduli) for (c0, c1) in pcols]
         per = len(units) // world  # = N / g
         self.units = [[u for u in units[r * per:(r + 1) * per] if u[2] > u[1]] for r in range(world)]
-        self.launches = []
-        for us in self.units:
-            merged = []
-            for j, c0, c1 in us:
-                if merged and merged[-1][0] == j and merged[-1][2] == c0:
-                    merged[-1] = (j, merged[-1][1], c1)
-                else:
-                    merged.append((j, c0, c1))
-            self.launches.append(merged)
-        self.mods = [((us[0][0], us[-1][0] + 1) if us else (0, 0)) for us in self.units]
         self.cols = blocks(n, world, align)
         self.rows = blocks(m, world, align)
+        self.launches = [self._schedule(r) for r in range(world)]
+        self.mods = [((us[0][0], us[-1][0] + 1) if us else (0, 0)) for us in self.units]
         self.stages = max((len(x) for x in self.launches), default=0)
+
+    def owners(self, c0, c1):
+        """[(owner, lo, hi)]: the output-column owners of the columns [c0, c1)"""
+        return [(s, max(c0, s0), min(c1, s1)) for s, (s0, s1) in enumerate(self.cols) if max(c0, s0) < min(c1, s1)]
+
+    def _schedule(self, r):
+        pieces = [(j, lo, hi, s) for j, c0, c1 in self.units[r] for s, lo, hi in self.owners(c0, c1)]
+        remote, local = [], []
+        for j, lo, hi, s in pieces:
+            if s != r:  # one modulus per launch, consecutive columns merged
+                if remote and remote[-1][0] == j and remote[-1][3] == lo:
+                    remote[-1] = (j, j + 1, remote[-1][2], hi)
+                else:
+                    remote.append((j, j + 1, lo, hi))
+            else:  # the same columns over consecutive moduli merged
+                if local and local[-1][1] == j and local[-1][2:] == (lo, hi):
+                    local[-1] = (local[-1][0], j + 1, lo, hi)
+                else:
+                    local.append((j, j + 1, lo, hi))
+        return remote + local
 
     def sends(self, r, t):
         """[(dst, j, c0, c1)]: residue column runs rank r sends after its launch t"""
         if t >= len(self.launches[r]):
             return []
-        j, a, b = self.launches[r][t]
-        out = []
-        for s, (s0, s1) in enumerate(self.cols):
-            lo, hi = max(a, s0), min(b, s1)
-            if s != r and lo < hi:
-                out.append((s, j, lo, hi))
-        return out
+        j0, j1, a, b = self.launches[r][t]
+        return [(s, j, lo, hi) for j in range(j0, j1) for s, lo, hi in self.owners(a, b) if s != r]
 
     def recvs(self, r, t):
         """[(src, j, c0, c1)]: residue column runs rank r receives in stage t"""
@@ -196,8 +208,8 @@ class HipShardOps:
         split(opA, opB, m, n, k, A, lda, B, ldb, N, fast, st["work"], st["dtype"], j0, j1, st["ct"],
               bound_ready=not fast, shifts_ready=fast)
 
-    def products(self, st, j, c0, c1):
-        products(st["m"], st["n"], st["k"], st["N"], st["work"], j, j + 1, st["ct"], cols=(c0, c1))
+    def products(self, st, j0, j1, c0, c1):
+        products(st["m"], st["n"], st["k"], st["N"], st["work"], j0, j1, st["ct"], cols=(c0, c1))
 
     def chunks(self, st, j, c0, c1):
         """uint8 views of the residue columns [c0, c1) of plane j (Karatsuba: one per sub-plane)"""
@@ -212,6 +224,11 @@ class HipShardOps:
         if c1 > c0:
             recombine(m, st["n"], st["k"], st["N"], 1.0, 0.0, Cb, m, st["work"], st["ct"], cols=(c0, c1))
         return Cb
+
+    def side_stream(self):
+        """a stream with no work of this call on it (receive-only transfer stages are posted from it)"""
+        dev = torch.cuda.current_device()
+        return self.cache.get(("side", dev), lambda: torch.cuda.Stream(device=dev))
 
     def sync(self):
         torch.cuda.current_stream().synchronize()
@@ -295,21 +312,32 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
         ops.encode(st, j0, j1)
     mark("encode")
 
-    # 3 + 4. products, each launch followed by the grouped transfers of its residue columns
+    # 3 + 4. products, each launch followed by the grouped transfers of its residue columns.  RCCL orders
+    # a call's transfers behind the work enqueued on the current stream so far: a stage that only
+    # receives (its buffers are columns no launch of this rank writes) is posted from a side stream so
+    # that it does not wait for this rank's remaining products
     reqs = []
     mine = plan.launches[rank]
+    side = None if host_sync else ops.side_stream()
+    if side is not None:
+        # ... but after everything enqueued before this call (the previous call's CRT reads these columns)
+        side.wait_stream(torch.cuda.current_stream())
     for t in range(plan.stages):
         if t < len(mine):
             ops.products(st, *mine[t])
-        p2p = []
-        for dst, j, a, b in plan.sends(rank, t):
-            p2p += [dist.P2POp(dist.isend, x, _global(group, dst), group) for x in ops.chunks(st, j, a, b)]
-        for src, j, a, b in plan.recvs(rank, t):
-            p2p += [dist.P2POp(dist.irecv, x, _global(group, src), group) for x in ops.chunks(st, j, a, b)]
-        if p2p:
-            if host_sync:
-                ops.sync()
-            reqs += dist.batch_isend_irecv(p2p)
+        snd = [dist.P2POp(dist.isend, x, _global(group, dst), group)
+               for dst, j, a, b in plan.sends(rank, t) for x in ops.chunks(st, j, a, b)]
+        rcv = [dist.P2POp(dist.irecv, x, _global(group, src), group)
+               for src, j, a, b in plan.recvs(rank, t) for x in ops.chunks(st, j, a, b)]
+        if not snd and not rcv:
+            continue
+        if host_sync:
+            ops.sync()
+        if snd or side is None:
+            reqs += dist.batch_isend_irecv(snd + rcv)
+        else:
+            with torch.cuda.stream(side):
+                reqs += dist.batch_isend_irecv(rcv)
     mark("products")
     for q in reqs:
         q.wait()

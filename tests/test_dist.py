@@ -89,8 +89,8 @@ class OracleShardOps:
     def encode(self, st, j0, j1):
         pass
 
-    def products(self, st, j, c0, c1):
-        st["R"][j, c0:c1] = torch.from_numpy(st["full"][j, c0:c1])
+    def products(self, st, j0, j1, c0, c1):
+        st["R"][j0:j1, c0:c1] = torch.from_numpy(st["full"][j0:j1, c0:c1])
 
     def chunks(self, st, j, c0, c1):
         return [st["R"][j, c0:c1].view(-1)]
