@@ -28,6 +28,15 @@ for step in "$@"; do
     gloo2)
       GEMMUL8_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 2 $arg > $OUT/gloo2_$i.json 2> $OUT/gloo2_$i.err
       rc=$?; cat $OUT/gloo2_$i.json ;;
+    gloo4)
+      GEMMUL8_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 $arg > $OUT/gloo4_$i.json 2> $OUT/gloo4_$i.err
+      rc=$?; cat $OUT/gloo4_$i.json ;;
+    profile)
+      timeout -k 10 900 bash tools/profile.sh $arg > $OUT/profile_$i.log 2>&1
+      rc=$?; tail -5 $OUT/profile_$i.log ;;
+    cmd)
+      timeout -k 10 600 bash -c "$arg" > $OUT/cmd_$i.log 2>&1
+      rc=$?; tail -20 $OUT/cmd_$i.log ;;
     *) echo "unknown step $name"; rc=2 ;;
   esac
   echo "[$(date +%T)] step $i rc=$rc"
