@@ -150,6 +150,21 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
  * with a wrong expectation, so every pair mismatches). */
 unsigned long long gemmul8_residue_selftest(void *stream, int path);
 
+/* Epilogue semantics of C = alpha * AB + beta * C, process-wide (default GEMMUL8_EPILOGUE_BLAS; the
+ * environment variable GEMMUL8_EPILOGUE=reference selects the other at load time).
+ *   GEMMUL8_EPILOGUE_BLAS       BLAS: beta = 0 never reads C; alpha = 1 with another beta is
+ *                               beta * C + AB; beta = 1 is alpha * AB + C at every moduli count.
+ *   GEMMUL8_EPILOGUE_REFERENCE  the reference's kernels bit for bit, its non-BLAS variants included
+ *                               (inverse_scaling.hpp): alpha = 1 with beta off {0, 1} computes beta * AB + C
+ *                               (_1b, :417, :682), alpha != 1 with beta = 1 at num_moduli >= 8 (two-level
+ *                               moduli, real and complex double output) computes alpha * C + AB (_2_a1,
+ *                               :736, :763), and alpha != 1 with beta = 0 reads C as fma(0, C, alpha * AB)
+ *                               (_ab, :522, :549, :791, :819: NaN / Inf in C propagate).
+ * Returns GEMMUL8_E_UNSUPPORTED for an unknown mode.  Takes effect for calls enqueued afterwards. */
+enum { GEMMUL8_EPILOGUE_BLAS = 0, GEMMUL8_EPILOGUE_REFERENCE = 1 };
+int gemmul8_set_epilogue(int mode);
+int gemmul8_get_epilogue(void);
+
 /* Name of the residue-product kernel the last products launch of this process took
  * ("gemm_i8_persistent_kernel", "gemm_i8_kernel", "gemm_i8_kernel (k-chunked)" or "none"). */
 const char *gemmul8_last_products_kernel(void);

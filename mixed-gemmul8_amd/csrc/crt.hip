@@ -32,6 +32,7 @@ struct CrtArgs {
     void *C;
     size_t ldc;
     double ar, ai, br, bi;
+    int ref_epi;  // 1: the reference's epilogue kernels including their non-BLAS variants (gemmul8_set_epilogue)
 };
 
 // CRT value of one element (inverse_scaling.hpp:35-62 numM = 1, :138-172 numM = 2) with the weights
@@ -92,21 +93,23 @@ __device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fas
 }
 
 // BLAS epilogue; the reference's alpha==1/beta==1 special cases are kept
-// (inverse_scaling.hpp:823-948), its non-BLAS variants (:417, :682, :736, :763) are not.
-__device__ __forceinline__ double epi_d(double v, double c, double al, double be) {
-    if (be == 0.0) return al == 1.0 ? v : al * v;  // C is not read (BLAS)
+// (inverse_scaling.hpp:823-948).  Its non-BLAS variants only with ref (the reference-epilogue mode):
+// _1b / _2_1b compute beta*AB + C (:417, :682), _2_a1 alpha*C + AB (:736, :763; two-level moduli only,
+// numM2), and _ab reads C at beta = 0 (fma(0, C, alpha*AB): NaN / Inf in C propagate, :522, :791).
+__device__ __forceinline__ double epi_d(double v, double c, double al, double be, bool ref, bool numM1) {
+    if (be == 0.0 && !(ref && al != 1.0)) return al == 1.0 ? v : al * v;  // C is not read (BLAS)
     if (al == 1.0) {
         if (be == 1.0) return c + v;
-        return __builtin_fma(be, c, v);
+        return ref ? __builtin_fma(be, v, c) : __builtin_fma(be, c, v);
     }
-    if (be == 1.0) return __builtin_fma(al, v, c);
+    if (be == 1.0) return (ref && !numM1) ? __builtin_fma(al, c, v) : __builtin_fma(al, v, c);
     return __builtin_fma(be, c, al * v);
 }
-__device__ __forceinline__ float epi_f(float v, float c, float al, float be) {
-    if (be == 0.0f) return al == 1.0f ? v : al * v;
+__device__ __forceinline__ float epi_f(float v, float c, float al, float be, bool ref) {
+    if (be == 0.0f && !(ref && al != 1.0f)) return al == 1.0f ? v : al * v;
     if (al == 1.0f) {
         if (be == 1.0f) return c + v;
-        return __builtin_fmaf(be, c, v);
+        return ref ? __builtin_fmaf(be, v, c) : __builtin_fmaf(be, c, v);
     }
     if (be == 1.0f) return __builtin_fmaf(al, v, c);
     return __builtin_fmaf(be, c, al * v);
@@ -129,12 +132,14 @@ template <> struct OutElem<3> { using T = float2; };
 template <int OT> struct BlasEpi;
 template <> struct BlasEpi<0> {
     template <bool NUMM1>
-    static __device__ __forceinline__ double f(double v, double c, const CrtArgs &a) { return epi_d(v, c, a.ar, a.br); }
+    static __device__ __forceinline__ double f(double v, double c, const CrtArgs &a) {
+        return epi_d(v, c, a.ar, a.br, a.ref_epi != 0, NUMM1);
+    }
 };
 template <> struct BlasEpi<1> {
     template <bool NUMM1>
     static __device__ __forceinline__ float f(float v, float c, const CrtArgs &a) {
-        return epi_f(v, c, (float)a.ar, (float)a.br);
+        return epi_f(v, c, (float)a.ar, (float)a.br, a.ref_epi != 0);
     }
 };
 // Complex outputs: the reference's kernels operation for operation (inverse_scaling.hpp:268-948), with
@@ -144,6 +149,8 @@ template <> struct BlasEpi<1> {
 //   beta = 1: hipCfma(alpha, v, C) (_a1);  otherwise hipCfma(beta, C, hipCmul(alpha, v)) (_ab).
 // Two departures, both BLAS semantics: beta = 0 does not read C (the reference's _ab does),
 // and alpha = 1 with another beta is hipCfma(beta, C, v) (the reference's _1b computes beta*AB + C, 10.3).
+// ref (the reference-epilogue mode) takes the reference's kernels there too, and its _2_a1 form
+// hipCfma(alpha, C, v) for beta = 1 at two moduli levels (NUMM2).
 template <typename R, typename R2, bool IM_PXQY> struct CplxEpi {
     static __device__ __forceinline__ R fma_(R a, R b, R c) {
         if constexpr (sizeof(R) == 8) return __builtin_fma(a, b, c);
@@ -159,10 +166,14 @@ template <typename R, typename R2, bool IM_PXQY> struct CplxEpi {
         R re = fma_(pr, qr, rr), im = fma_(qr, pi, ri);
         return mk(fma_(-pi, qi, re), fma_(pr, qi, im));
     }
-    static __device__ __forceinline__ R2 f(R2 v, R2 c, R ar, R ai, R br, R bi) {
+    static __device__ __forceinline__ R2 f(R2 v, R2 c, R ar, R ai, R br, R bi, bool ref, bool numM1) {
         const bool a1 = ar == R(1) && ai == R(0);
-        if (br == R(0) && bi == R(0)) return a1 ? v : cmul(ar, ai, v.x, v.y);
-        if (br == R(1) && bi == R(0)) return a1 ? mk(c.x + v.x, c.y + v.y) : cfma(ar, ai, v.x, v.y, c.x, c.y);
+        if (br == R(0) && bi == R(0) && !(ref && !a1)) return a1 ? v : cmul(ar, ai, v.x, v.y);
+        if (br == R(1) && bi == R(0)) {
+            if (a1) return mk(c.x + v.x, c.y + v.y);
+            return (ref && !numM1) ? cfma(ar, ai, c.x, c.y, v.x, v.y) : cfma(ar, ai, v.x, v.y, c.x, c.y);
+        }
+        if (a1 && ref) return cfma(br, bi, v.x, v.y, c.x, c.y);  // _1b: beta * AB + C
         const R2 x = a1 ? v : cmul(ar, ai, v.x, v.y);
         return cfma(br, bi, c.x, c.y, x.x, x.y);
     }
@@ -172,13 +183,14 @@ template <typename R, typename R2, bool IM_PXQY> struct CplxEpi {
 template <> struct BlasEpi<2> {
     template <bool NUMM1>
     static __device__ __forceinline__ double2 f(double2 v, double2 c, const CrtArgs &a) {
-        return CplxEpi<double, double2, !NUMM1>::f(v, c, a.ar, a.ai, a.br, a.bi);
+        return CplxEpi<double, double2, !NUMM1>::f(v, c, a.ar, a.ai, a.br, a.bi, a.ref_epi != 0, NUMM1);
     }
 };
 template <> struct BlasEpi<3> {
     template <bool NUMM1>
     static __device__ __forceinline__ float2 f(float2 v, float2 c, const CrtArgs &a) {
-        return CplxEpi<float, float2, false>::f(v, c, (float)a.ar, (float)a.ai, (float)a.br, (float)a.bi);
+        return CplxEpi<float, float2, false>::f(v, c, (float)a.ar, (float)a.ai, (float)a.br, (float)a.bi,
+                                                a.ref_epi != 0, true);
     }
 };
 
@@ -245,7 +257,8 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     const size_t r0 = wrow0 + (size_t)lane * CRT_ROWS;
     const int nr = r0 >= a.m ? 0 : (a.m - r0 >= CRT_ROWS ? CRT_ROWS : (int)(a.m - r0));
     const bool plain_ab = a.ar == 1.0 && a.ai == 0.0 && a.br == 0.0 && a.bi == 0.0;
-    const bool zero_beta = a.br == 0.0 && a.bi == 0.0;
+    // C is not read at beta = 0 (BLAS), except by the reference's _ab kernels (reference-epilogue mode)
+    const bool zero_beta = a.br == 0.0 && a.bi == 0.0 && !(a.ref_epi && !(a.ar == 1.0 && a.ai == 0.0));
     int16_t sa[CRT_ROWS];
 #pragma unroll
     for (int e = 0; e < CRT_ROWS; ++e) sa[e] = e < nr ? a.sftA[r0 + e] : 0;
@@ -343,8 +356,9 @@ static void launch_crt(const CrtArgs &a, unsigned N, dim3 grid, hipStream_t st) 
 }
 
 void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const int16_t *sftB, const CrtParams &CP,
-                 OutType ot, const void *alpha, const void *beta, void *C, size_t ldc, hipStream_t st) {
+                 OutType ot, const void *alpha, const void *beta, void *C, size_t ldc, hipStream_t st, int ref_epi) {
     CrtArgs a{};
+    a.ref_epi = ref_epi;
     a.R = R;
     a.planeR = L.planeR;
     a.ldr = L.ldr;

@@ -12,6 +12,7 @@
 // caller's stream by events, so the two operands' split kernels overlap where either one alone
 // leaves the chip idle (small or strided operands); the join precedes everything that reads
 // both.  Events only: the call stays asynchronous and graph-capturable.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
@@ -358,19 +359,27 @@ static void phase_products(const Views &v, unsigned N, unsigned j0, unsigned j1,
             nullptr, sub_mod_params(N, j0, j1), st, queue_of(v, j0), queue_zeroed);
 }
 
+// epilogue mode of the process (gemmul8_set_epilogue): 0 BLAS semantics (default), 1 the reference's
+// epilogue kernels including their non-BLAS variants; GEMMUL8_EPILOGUE=reference sets 1 at load time
+static std::atomic<int> g_epilogue_mode{[] {
+    const char *e = getenv("GEMMUL8_EPILOGUE");
+    return (e && (e[0] == 'r' || e[0] == '1')) ? 1 : 0;
+}()};
+
 // phase 3: CRT + scaling + BLAS epilogue over all N residue planes; columns [c0, c1) of the output only
 // when given (C then points at column c0): the residue planes are column-major, so a column range is
 // the same kernel over an offset plane base, sftB + c0 and n = c1 - c0
 static void phase_crt(const Views &v, unsigned N, OutType ot, const void *alpha, const void *beta, void *C, size_t ldc,
                       hipStream_t st, size_t c0 = 0, size_t c1 = SIZE_MAX) {
     const CrtParams CP = make_crt_params(N, ot == OutType::F32 || ot == OutType::C32);
+    const int ref_epi = g_epilogue_mode.load(std::memory_order_relaxed);
     if (c0 == 0 && c1 >= v.L.n) {
-        crt_inverse(v.R, v.L, v.sftA, v.sftB, CP, ot, alpha, beta, C, ldc, st);
+        crt_inverse(v.R, v.L, v.sftA, v.sftB, CP, ot, alpha, beta, C, ldc, st, ref_epi);
         return;
     }
     Layout L = v.L;
     L.n = c1 - c0;
-    crt_inverse(v.R + c0 * L.ldr, L, v.sftA, v.sftB + c0, CP, ot, alpha, beta, C, ldc, st);
+    crt_inverse(v.R + c0 * L.ldr, L, v.sftA, v.sftB + c0, CP, ot, alpha, beta, C, ldc, st, ref_epi);
 }
 
 // phase 2 over the columns [c0, c1) of the residue planes only (c0 a multiple of TILE, c1 one too or n):
@@ -736,6 +745,14 @@ int gemmul8_i8_product_raw(void *stream, size_t m, size_t n, size_t k, unsigned 
                  static_cast<hipStream_t>(stream));
     return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
+
+int gemmul8_set_epilogue(int mode) {
+    if (mode != GEMMUL8_EPILOGUE_BLAS && mode != GEMMUL8_EPILOGUE_REFERENCE) return GEMMUL8_E_UNSUPPORTED;
+    oz2::g_epilogue_mode.store(mode, std::memory_order_relaxed);
+    return GEMMUL8_OK;
+}
+
+int gemmul8_get_epilogue(void) { return oz2::g_epilogue_mode.load(std::memory_order_relaxed); }
 
 const char *gemmul8_last_products_kernel(void) {
     switch (oz2::g_last_residue_kernel.load(std::memory_order_relaxed)) {

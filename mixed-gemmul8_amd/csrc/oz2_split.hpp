@@ -106,7 +106,8 @@ unsigned long long residue_selftest(int path, hipStream_t st);
 
 // ---- crt.hip ----
 enum class OutType : int { F64 = 0, F32 = 1, C64 = 2, C32 = 3 };
+// ref_epi: 1 = the reference's epilogue kernels including their non-BLAS variants (gemmul8_set_epilogue)
 void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const int16_t *sftB, const CrtParams &CP,
-                 OutType ot, const void *alpha, const void *beta, void *C, size_t ldc, hipStream_t st);
+                 OutType ot, const void *alpha, const void *beta, void *C, size_t ldc, hipStream_t st, int ref_epi);
 
 }  // namespace oz2

@@ -59,6 +59,10 @@ def _load():
     lib.gemmul8_randmat.argtypes = [p, i, sz, sz, p, ctypes.c_double, ctypes.c_ulonglong]
     lib.gemmul8_dd_gemm.argtypes = [p, sz, sz, sz, p, p, p, p]
     lib.gemmul8_relerr_dd.argtypes = [p, sz, p, p, p, p]
+    lib.gemmul8_set_epilogue.argtypes = [i]
+    lib.gemmul8_set_epilogue.restype = i
+    lib.gemmul8_get_epilogue.argtypes = []
+    lib.gemmul8_get_epilogue.restype = i
     lib.gemmul8_last_products_kernel.restype = ctypes.c_char_p
     lib.gemmul8_last_products_kernel.argtypes = []
     lib.gemmul8_mfma_ceiling.restype = ctypes.c_double
@@ -286,6 +290,22 @@ def relerr_dd(C, C1, C2, stream=None):
     cnt = s.numel()
     med = s[cnt // 2] if cnt & 1 else (s[cnt // 2] + s[cnt // 2 - 1]) * 0.5
     return float(s[-1]), float(med)
+
+
+EPILOGUE_BLAS, EPILOGUE_REFERENCE = 0, 1
+
+
+def set_epilogue(mode):
+    """Epilogue semantics for later calls: "blas" (default) or "reference" (the reference's kernels bit for bit,
+    their non-BLAS alpha / beta variants included; include/gemmul8_c.h).  Returns the previous mode's name."""
+    names = {"blas": EPILOGUE_BLAS, "reference": EPILOGUE_REFERENCE}
+    prev = get_epilogue()
+    _check(lib.gemmul8_set_epilogue(names[mode] if isinstance(mode, str) else int(mode)))
+    return prev
+
+
+def get_epilogue():
+    return "reference" if lib.gemmul8_get_epilogue() == EPILOGUE_REFERENCE else "blas"
 
 
 def last_products_kernel():

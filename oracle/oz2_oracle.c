@@ -575,20 +575,31 @@ static float epi_f(float v, float c, float al, float be, int quirks) {
  * (fma(-p.y, q.y, fma(p.x, q.x, r.x)), fma(p.x, q.y, fma(q.x, p.y, r.y))) as clang contracts them
  * (inverse_scaling.hpp:268-948): alpha = 1, beta = 0: v; alpha = beta = 1: C + v (CAdd); beta = 1:
  * hipCfma(alpha, v, C); otherwise hipCfma(beta, C, hipCmul(alpha, v)).  BLAS departures as the GPU
- * build: beta = 0 does not read C, alpha = 1 with another beta is hipCfma(beta, C, v). */
+ * build: beta = 0 does not read C, alpha = 1 with another beta is hipCfma(beta, C, v).  With quirks the
+ * reference's kernels there too: _1b hipCfma(beta, v, C) (:443, :709), _2_a1 hipCfma(alpha, C, v) for the
+ * two-level (IM_F64) kernels (:763), and _ab at beta = 0 (the caller passes C). */
 #define OZ2O_CEPI(NAME, R, FMA)                                                                              \
-    static void NAME(R vr, R vi, R cr, R ci, R ar, R ai, R br, R bi, R *outr, R *outi, int IM_F64) {        \
+    static void NAME(R vr, R vi, R cr, R ci, R ar, R ai, R br, R bi, R *outr, R *outi, int IM_F64,          \
+                     int quirks) {                                                                            \
         int a1 = ar == (R)1 && ai == (R)0;                                                                    \
         R xr = vr, xi = vi;                                                                                   \
         if (!a1) {                                                                                            \
             xr = FMA(ar, vr, -(ai * vi));                                                                     \
             xi = IM_F64 ? FMA(ar, vi, ai * vr) : FMA(ai, vr, ar * vi);                                        \
         }                                                                                                     \
-        if (br == (R)0 && bi == (R)0) { *outr = xr; *outi = xi; return; }                                   \
+        if (br == (R)0 && bi == (R)0 && !(quirks && !a1)) { *outr = xr; *outi = xi; return; }               \
         if (br == (R)1 && bi == (R)0) {                                                                       \
             if (a1) { *outr = cr + vr; *outi = ci + vi; return; }                                             \
+            if (quirks && IM_F64) {                                                                           \
+                R re = FMA(ar, cr, vr), im = FMA(cr, ai, vi);                                                 \
+                *outr = FMA(-ai, ci, re); *outi = FMA(ar, ci, im); return;                                    \
+            }                                                                                                 \
             R re = FMA(ar, vr, cr), im = FMA(vr, ai, ci);                                                     \
             *outr = FMA(-ai, vi, re); *outi = FMA(ar, vi, im); return;                                        \
+        }                                                                                                     \
+        if (a1 && quirks) {                                                                                   \
+            R re = FMA(br, vr, cr), im = FMA(vr, bi, ci);                                                     \
+            *outr = FMA(-bi, vi, re); *outi = FMA(br, vi, im); return;                                        \
         }                                                                                                     \
         R re = FMA(br, cr, xr), im = FMA(cr, bi, xi);                                                         \
         *outr = FMA(-bi, ci, re); *outi = FMA(br, ci, im);                                                    \
@@ -623,15 +634,16 @@ int oz2o_crt(char tc, int complex_bm, size_t m, size_t n, unsigned N, const uint
                 if (tc == 'z') {
                     const double *al = (const double *)alpha, *be = (const double *)beta;
                     double *Cz = (double *)C;
-                    int zb = be[0] == 0.0 && be[1] == 0.0;
+                    int zb = be[0] == 0.0 && be[1] == 0.0 && !(quirks && !(al[0] == 1.0 && al[1] == 0.0));
                     double cr = zb ? 0.0 : Cz[2 * o], ci = zb ? 0.0 : Cz[2 * o + 1];
-                    cepi_d(vr, vi, cr, ci, al[0], al[1], be[0], be[1], &Cz[2 * o], &Cz[2 * o + 1], !numM1);
+                    cepi_d(vr, vi, cr, ci, al[0], al[1], be[0], be[1], &Cz[2 * o], &Cz[2 * o + 1], !numM1, quirks);
                 } else {
                     const float *al = (const float *)alpha, *be = (const float *)beta;
                     float *Cc = (float *)C;
-                    int zb = be[0] == 0.0f && be[1] == 0.0f;
+                    int zb = be[0] == 0.0f && be[1] == 0.0f && !(quirks && !(al[0] == 1.0f && al[1] == 0.0f));
                     float cr = zb ? 0.0f : Cc[2 * o], ci = zb ? 0.0f : Cc[2 * o + 1];
-                    cepi_f((float)vr, (float)vi, cr, ci, al[0], al[1], be[0], be[1], &Cc[2 * o], &Cc[2 * o + 1], 0);
+                    cepi_f((float)vr, (float)vi, cr, ci, al[0], al[1], be[0], be[1], &Cc[2 * o], &Cc[2 * o + 1], 0,
+                           quirks);
                 }
             }
         }

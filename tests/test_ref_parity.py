@@ -256,6 +256,7 @@ def test_complex_alpha_beta_same_bits(case):
     dict(seed=101, extreme=False, ab_mode="general", ld=False),
     dict(seed=102, extreme=False, ab_mode="general", ld=True),
     dict(seed=103, extreme=True, ab_mode="general", ld=False),
+    dict(seed=104, extreme=True, ab_mode="general", ld=False, ref_epi=True),
 ])
 def test_randomized_live_parity(mode):
     """tools/probes/fuzz_ref.py as a test: 300 random calls (the 12 type combinations, N = 2..20, both modes,
@@ -266,6 +267,65 @@ def test_randomized_live_parity(mode):
     sys.path.insert(0, os.path.join(ROOT, "tools", "probes"))
     import fuzz_ref
     out = fuzz_ref.sweep(300, mode["seed"], extreme=mode["extreme"], ab_mode=mode["ab_mode"], ld=mode["ld"],
-                         verbose=False)
+                         verbose=False, ref_epi=mode.get("ref_epi", False))
     assert out["cases"] == 300
     assert not out["failures"], out["failures"][:3]
+
+
+# (type, num_moduli, alpha, beta, NaN / Inf in C): the reference's non-BLAS epilogue variants (DESIGN.md 10.3,
+# 10.16), which the default BLAS mode does not reproduce: alpha = 1 with beta off {0, 1} (_1b), alpha != 1 with
+# beta = 1 at two moduli levels (_2_a1), alpha != 1 with beta = 0 reading C (_ab); one- and two-level moduli
+@pytest.mark.parametrize("case", [
+    ("d", 6, 1.0, 0.5, False), ("d", 14, 1.0, -0.75, False), ("d", 14, 2.5, 1.0, False), ("d", 6, 2.5, 1.0, False),
+    ("d", 14, 2.5, 0.0, True), ("d", 9, -1.5, 0.0, False), ("s", 8, 1.0, 0.5, False), ("s", 12, 2.5, 0.0, True),
+    ("s", 10, 2.5, 1.0, False),
+    ("z", 6, 1.0, 0.25 + 0.75j, False), ("z", 14, 1.0, -1.25 + 0.5j, False), ("z", 14, 1.5 - 0.5j, 1.0, False),
+    ("z", 6, 1.5 - 0.5j, 1.0, False), ("z", 14, 0.3 + 1.7j, 0.0, True), ("z", 12, 2.5, 0.0, False),
+    ("c", 8, 1.0, 0.25 + 0.75j, False), ("c", 12, 1.5 - 0.5j, 1.0, False), ("c", 10, 0.3 + 1.7j, 0.0, True),
+])
+def test_reference_epilogue_mode_same_bits(case):
+    """gemmul8_set_epilogue(GEMMUL8_EPILOGUE_REFERENCE): the reference's epilogue kernels bit for bit, including
+    the alpha / beta classes where they depart from BLAS; the same call in the default mode follows BLAS and
+    differs there; the CPU oracle with quirks=True restates the same bits"""
+    import torch
+    import gemmul8 as G
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    t, N, al, be, nonfinite = case
+    m, n, k = 150, 130, 256
+    lib = _ref()
+    cplx = t in "zc"
+    ct = 1 if cplx else 0
+    tdt = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}[t]
+    npt = {"d": np.float64, "s": np.float32, "z": np.complex128, "c": np.complex64}[t]
+    A = G.randmat(m, k, tdt, 0.5, 123456)
+    B = G.randmat(k, n, tdt, 0.5, 654321)
+    C0 = G.randmat(m, n, tdt, 0.5, 777)
+    if nonfinite:
+        C0[4, 3] = float("inf")
+        C0[9, 11] = float("nan")
+        C0[2, 5] = -0.0
+    C_ref, C_new, C_blas = C0.clone(), C0.clone(), C0.clone()
+    alpha, beta = np.array([al], npt), np.array([be], npt)
+    wref = torch.zeros(lib.ref_work_size(m, n, k, N, ct) + (1 << 22), dtype=torch.uint8, device="cuda")
+    rc = lib.ref_gemm(CODES[t], CODES[t], CODES[t], 0, 0, m, n, k, alpha.ctypes.data, A.data_ptr(), m, B.data_ptr(), k,
+                      beta.ctypes.data, C_ref.data_ptr(), m, N, 1, ct, wref.data_ptr(), None)
+    assert rc == 0
+    a, b = (complex(al), complex(be)) if cplx else (float(al.real if isinstance(al, complex) else al), float(be))
+    work = G.alloc_work(m, n, k, N, ct)
+    prev = G.set_epilogue("reference")
+    try:
+        assert G.get_epilogue() == "reference"
+        G.gemm(0, 0, m, n, k, a, A, m, B, k, b, C_new, m, N, True, work, ct)
+    finally:
+        G.set_epilogue(prev)
+    G.gemm(0, 0, m, n, k, a, A, m, B, k, b, C_blas, m, N, True, work, ct)
+    torch.cuda.synchronize()
+    nbad = int((C_ref.view(torch.uint8) != C_new.view(torch.uint8)).sum())
+    assert nbad == 0, f"{nbad} bytes differ from the reference in reference-epilogue mode"
+    Co = O.gemm(A.cpu().numpy().T, B.cpu().numpy().T, N, True, npt, al, be, C0.cpu().numpy().T, quirks=True)
+    assert np.asfortranarray(Co).tobytes() == C_new.cpu().numpy().T.tobytes(order="F")
+    numM2 = N >= 8 and t in "dz"
+    departs = (al == 1 and be not in (0, 1)) or (al != 1 and be == 1 and numM2) or (al != 1 and be == 0 and nonfinite)
+    if departs:
+        assert not torch.equal(C_blas.view(torch.uint8), C_new.view(torch.uint8))

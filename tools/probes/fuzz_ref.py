@@ -28,13 +28,14 @@ AB = os.environ.get("FUZZ_AB", "basic")
 LD = os.environ.get("FUZZ_LD") == "1"  # padded leading dimensions (not with FUZZ_EXTREME)  # "general": complex and general (alpha, beta) too  # half the cases with extreme / non-finite inputs
 
 
-def defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab):
-    """the reference-defect classes of DESIGN.md section 10 (None: a clean case)"""
+def defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab, ref_epi=False):
+    """the reference-defect classes of DESIGN.md section 10 (None: a clean case); ref_epi: the library runs in
+    its reference-epilogue mode, which reproduces the 10.3 variants"""
     cplx = ta in "cz"
     al, be = ab
-    if al == 1 and be not in (0, 1):
+    if al == 1 and be not in (0, 1) and not ref_epi:
         return "10.3 (_1b)"
-    if al != 1 and be == 1 and tc in "dz":
+    if al != 1 and be == 1 and tc in "dz" and not ref_epi:
         return "10.3 (_2_a1)"  # (numM = 2 for most N; kept out wholesale)
     if cplx and ct in (2, 3) and (tc == "z" and N > 7):
         return "10.5"
@@ -61,8 +62,18 @@ def defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab):
     return None
 
 
-def sweep(cases, seed, mn=None, kr=None, extreme=None, ab_mode=None, ld=None, verbose=True):
-    """run `cases` random calls through both libraries; returns the summary dict (failures first)"""
+def sweep(cases, seed, mn=None, kr=None, extreme=None, ab_mode=None, ld=None, verbose=True, ref_epi=False):
+    """run `cases` random calls through both libraries; returns the summary dict (failures first).
+    ref_epi: the library in its reference-epilogue mode (gemmul8.set_epilogue), alpha / beta drawn from
+    every kernel class including the non-BLAS ones, beta = 0 with alpha != 1 also with non-finite C"""
+    prev = G.set_epilogue("reference" if ref_epi else "blas")
+    try:
+        return _sweep(cases, seed, mn, kr, extreme, ab_mode, ld, verbose, ref_epi)
+    finally:
+        G.set_epilogue(prev)
+
+
+def _sweep(cases, seed, mn, kr, extreme, ab_mode, ld, verbose, ref_epi):
     global MN, K, EXTREME, AB, LD
     MN, K = mn or MN, kr or K
     EXTREME = EXTREME if extreme is None else extreme
@@ -86,11 +97,13 @@ def sweep(cases, seed, mn=None, kr=None, extreme=None, ab_mode=None, ld=None, ve
             if cplx:
                 pool += [(1.5 - 0.5j, 0.0), (1.5 - 0.5j, 0.25 + 0.75j), (1.0 + 1.0j, 1.0), (2.5, -0.5j),
                          (0.3 + 1.7j, -1.25 + 0.5j), (0.3 + 1.7j, 0.0), (-0.7 + 0.9j, 1.0)]  # inexact ai * x
+            if ref_epi:  # the non-BLAS kernels: _1b (alpha = 1, another beta)
+                pool += [(1.0, 0.5), (1.0, -1.75)] + ([(1.0, 0.25 + 0.75j)] if cplx else [])
             ab = pool[rng.integers(len(pool))]
         else:
             ab = [(1.0, 0.0), (1.0, 1.0), (2.5, 0.0)][rng.integers(3)]
         phi = float(rng.choice([0.5, 1.0, 2.0]))
-        why = defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab)
+        why = defect(ta, tb, tc, m, n, k, N, fast, ct, opA, opB, ab, ref_epi)
         if why:
             skipped[why] = skipped.get(why, 0) + 1
             continue
@@ -112,7 +125,7 @@ def sweep(cases, seed, mn=None, kr=None, extreme=None, ab_mode=None, ld=None, ve
         B = G.randmat(ldb, k if opB else n, TDT[tb], phi, seed + 1)
         special = EXTREME and not LD and rng.random() < 0.5
         inj = []
-        if special and ab[0] != 1 and ab[1] == 0:  # the reference's _ab reads C at beta = 0: zero signs
+        if special and ab[0] != 1 and ab[1] == 0 and not ref_epi:  # the reference's _ab reads C at beta = 0
             skipped["10.16"] = skipped.get("10.16", 0) + 1
             continue
         if special:  # extreme vectors (test_ref_parity._extreme) and scattered NaN / +-Inf
