@@ -49,7 +49,7 @@ import math
 import torch
 import torch.distributed as dist
 
-from . import (OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, gemm, layout, split, split_bound,
+from . import (OP_N, OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, gemm, layout, split, split_bound,
                products, recombine, shard_stats, shard_bound)
 
 TILE = 256  # product tile edge: column blocks of the product units start at multiples of it
