@@ -50,7 +50,7 @@ WORKLOADS = {
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--no-dgemm", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=0, help="CPU baseline size (default: auto)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def _free_port():
@@ -77,15 +77,22 @@ def _free_port():
     return p
 
 
+def launch_command(args, argv):
+    """the torch.distributed.run command line of a --gpus N > 1 run started outside torchrun (None: run here)"""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+
+
 def maybe_launch(args):
     """--gpus N > 1 outside torchrun: run N ranks under torch.distributed.run as a child (no GPU touched
     in this process) and exit with its status."""
-    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+    cmd = launch_command(args, sys.argv[1:])
+    if cmd is None:
         return
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
     sys.exit(subprocess.call(cmd, env=env))
 
 
@@ -204,6 +211,34 @@ def make_operands(kind, m, n, k, seed_a, dev):
     return G.randmat(m, k, torch.float64, 0.5, seed_a, dev), G.randmat(k, n, tb, 0.5, 123456, dev), torch.float64
 
 
+def select_workload(args, world):
+    """the configuration this run measures: --workload, else cfg2 on one GPU and cfg3 (the moduli-sharded
+    BASELINE config) on more; --size / --moduli / --accurate make it a custom one"""
+    name = args.workload or ("cfg3" if (world > 1 and args.partition == "moduli") else "cfg2")
+    wl = WORKLOADS[name]
+    m = args.size or wl["size"]
+    N = args.moduli or wl["moduli"]
+    fast = not (args.accurate or wl["accurate"])
+    custom = m != wl["size"] or N != wl["moduli"] or fast == wl["accurate"]
+    return {"name": name, "wl": wl, "m": m, "N": N, "fast": fast, "kind": wl["kind"], "custom": custom}
+
+
+def labels(W):
+    """(config.workload, metric) of a run: BASELINE.json's metric string only for the cfg2 workload itself"""
+    cplx, m, N, fast = W["kind"] == "z", W["m"], W["N"], W["fast"]
+    if W["custom"]:
+        workload = (f"{'complex ' if cplx else ''}{'mixed ' if W['kind'] == 'dfd' else ''}DGEMM emulation m=n=k={m}, "
+                    f"num_moduli={N}, {'fast' if fast else 'accurate'} mode")
+    else:
+        workload = W["wl"]["text"]
+    if W["name"] == "cfg2" and not W["custom"]:
+        metric = BASELINE_METRIC
+    else:
+        metric = (f"emulated {'ZGEMM' if cplx else 'DGEMM'} TFLOP/s + max rel-error, m=n=k={m} num_moduli={N}" +
+                  ("" if fast else " accurate") + (f" ({W['name']})" if not W["custom"] else ""))
+    return workload, metric
+
+
 def main():
     args = parse()
     maybe_launch(args)
@@ -211,13 +246,9 @@ def main():
     import gemmul8 as G
     from gemmul8 import dist as GD
 
-    wl_name = args.workload or ("cfg3" if (world > 1 and args.partition == "moduli") else "cfg2")
-    wl = WORKLOADS[wl_name]
-    m = n = k = args.size or wl["size"]
-    N = args.moduli or wl["moduli"]
-    fast = not (args.accurate or wl["accurate"])
-    kind = wl["kind"]
-    custom = (m != wl["size"] or N != wl["moduli"] or fast == wl["accurate"])
+    W = select_workload(args, world)
+    wl_name, wl, m, N, fast, kind, custom = W["name"], W["wl"], W["m"], W["N"], W["fast"], W["kind"], W["custom"]
+    n = k = m
     cplx = kind == "z"
     ct = G.COMPLEX_BIG_MATRIX_ENCODE if cplx else G.REAL_DEFAULT
     flop_per = (8.0 if cplx else 2.0) * m * n * k
@@ -337,14 +368,7 @@ def main():
             extra["rocblas_dgemm_tflops_1gpu"] = round(dg, 2)
             extra["vs_rocblas_dgemm_1gpu"] = round(value / dg, 3)
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev)
-        if custom:
-            workload = (f"{'complex ' if cplx else ''}{'mixed ' if kind == 'dfd' else ''}DGEMM emulation m=n=k={m}, "
-                        f"num_moduli={N}, {'fast' if fast else 'accurate'} mode")
-        else:
-            workload = wl["text"]
-        metric = BASELINE_METRIC if (wl_name == "cfg2" and not custom) else \
-            f"emulated {'ZGEMM' if cplx else 'DGEMM'} TFLOP/s + max rel-error, m=n=k={m} num_moduli={N}" + \
-            ("" if fast else " accurate") + (f" ({wl_name})" if not custom else "")
+        workload, metric = labels(W)
         out = {
             "metric": metric,
             "value": round(value, 3),

@@ -343,3 +343,25 @@ def test_dist_three_ranks_on_one_gpu_gloo():
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     assert "RESULT OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+def test_cfg3_size_moduli_shards_simulated_8_ranks():
+    """BASELINE cfg3 at full size (16384^3, 14 moduli, fast mode, the reference driver's inputs) through the
+    8-rank (modulus, column block) data flow, each simulated rank with its own workspace (8 x 11.5 GiB): the
+    assembled C is bit-identical to one gemmul8_gemm call"""
+    import torch
+    import gemmul8 as G
+    m = n = k = 16384
+    N = 14
+    A = G.randmat(m, k, torch.float64, 0.5, 123456)  # column-major m x k, op N (bench.py's cfg3 operands)
+    B = G.randmat(k, n, torch.float64, 0.5, 123456)
+    ref = torch.empty((n, m), dtype=torch.float64, device="cuda")
+    work = G.alloc_work(m, n, k, N)
+    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, ref, m, N, True, work)
+    torch.cuda.synchronize()
+    del work
+    got, plan = _simulate_moduli_shards(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, True, torch.float64, G.REAL_DEFAULT, 8)
+    assert [len(x) for x in plan.units] == [7] * 8
+    assert torch.equal(got.view(torch.uint8), ref.view(torch.uint8))
+    del got
+    torch.cuda.empty_cache()
