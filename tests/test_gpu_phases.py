@@ -365,3 +365,35 @@ def test_cfg3_size_moduli_shards_simulated_8_ranks():
     assert torch.equal(got.view(torch.uint8), ref.view(torch.uint8))
     del got
     torch.cuda.empty_cache()
+
+
+def test_moduli_column_shards_randomized():
+    """40 random calls through the simulated (modulus, column block) data flow: random shapes (m, n up to
+    1300, k up to 1500), num_moduli 2..20, 2..8 ranks, real f64 / f32 / mixed f64 x f32 / complex, fast and
+    accurate, ops N / T (and C for complex) -- each bit-identical to the single call"""
+    import torch
+    import gemmul8 as G
+    rng = np.random.default_rng(2027)
+    tdts = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}
+    for case in range(40):
+        ta = tb = "dszc"[int(rng.integers(4))]
+        if ta == "d" and rng.random() < 0.3:
+            tb = "s"
+        cplx = ta in "zc"
+        m, n, k = (int(rng.integers(1, 1300)), int(rng.integers(1, 1300)), int(rng.integers(1, 1500)))
+        N = int(rng.integers(2, 21))
+        world = int(rng.integers(2, 9))
+        fast = bool(rng.integers(2))
+        if cplx and not fast and N > 17:
+            N = 17
+        opA, opB = int(rng.integers(3 if cplx else 2)), int(rng.integers(3 if cplx else 2))
+        ct = G.COMPLEX_BIG_MATRIX_ENCODE if cplx else G.REAL_DEFAULT
+        out_dtype = tdts["z" if cplx and "z" in (ta, tb) else ("d" if "d" in (ta, tb) else ta)]
+        A = (_rand(k, m, 100 + case, tdts[ta]) if opA == 0 else _rand(m, k, 100 + case, tdts[ta]))
+        B = (_rand(n, k, 200 + case, tdts[tb]) if opB == 0 else _rand(k, n, 200 + case, tdts[tb]))
+        lda, ldb = (m if opA == 0 else k), (k if opB == 0 else n)
+        ref = torch.empty((n, m), dtype=out_dtype, device="cuda")
+        G.gemm(opA, opB, m, n, k, 1.0, A, lda, B, ldb, 0.0, ref, m, N, fast, G.alloc_work(m, n, k, N, ct), ct)
+        got, _ = _simulate_moduli_shards(opA, opB, m, n, k, A, lda, B, ldb, N, fast, out_dtype, ct, world)
+        torch.cuda.synchronize()
+        assert _same(got, ref), dict(case=case, types=ta + tb, m=m, n=n, k=k, N=N, W=world, fast=fast, op=(opA, opB))
