@@ -140,6 +140,8 @@ def _worker(rank, world, port, case, outdir):
     (3, (90, 30, 70, 9, False, np.float64)),
     (4, (100, 70, 64, 14, True, np.float64)),
     (2, (40, 50, 60, 6, True, np.complex128)),
+    (8, (120, 300, 64, 14, True, np.float64)),  # the cfg3 plan: 14 moduli, 8 ranks, 7 units each
+    (8, (60, 130, 40, 9, False, np.float64)),
 ])
 def test_sharded_equals_single_call(tmp_path, world, case):
     sys.path.insert(0, ROOT)
