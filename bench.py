@@ -65,6 +65,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--no-dgemm", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="sharded runs: skip timing the other partitions")
     ap.add_argument("--cpu-sample", type=int, default=0, help="CPU baseline size (default: auto)")
     return ap.parse_args(argv)
 
@@ -211,6 +212,53 @@ def make_operands(kind, m, n, k, seed_a, dev):
     return G.randmat(m, k, torch.float64, 0.5, seed_a, dev), G.randmat(k, n, tb, 0.5, 123456, dev), torch.float64
 
 
+def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
+    """SURVEY.md 8(e)'s partitions side by side, after the timed region, same operands (a few steps each):
+    the default (modulus, column block) units with C gathered on the root; whole moduli per rank with the residue
+    planes sent to the root and the root's CRT (variant (i)); row blocks of C, all moduli per rank, no exchange
+    (variant (ii), strong scaling); and the communication alone of the north-star's reduce of FP64 partial CRT
+    sums (two m x n double accumulators to the root; not bit-identical, so not built)."""
+    import torch.distributed as dist
+    steps, warm = 3, 1
+
+    def timed(fn):
+        try:
+            for _ in range(warm):
+                fn()
+            barrier(world)
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                fn()
+            barrier(world)
+        except Exception as e:  # a variant must not cost the main line (e.g. a collective the backend lacks)
+            return f"failed: {type(e).__name__}: {str(e)[:200]}"
+        return reduce_max(time.perf_counter() - t0, world) / steps * 1e3
+
+    out = {}
+    out["moduli_columns_gathered"] = timed(
+        lambda: GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, gather=True, ops=ops))
+    out["moduli_whole_planes_to_root"] = timed(
+        lambda: GD.gemm_moduli_planes_to_root(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, ops=ops))
+    r0, r1 = GD.blocks(m, world)[rank]
+    if r1 > r0:
+        wr = G.alloc_work(r1 - r0, n, k, N, G.REAL_DEFAULT, A.device)
+        Cr = torch.empty((n, r1 - r0), dtype=torch.float64, device=A.device)
+        Ar = A[:, r0:]  # rows r0.. of the column-major A (lda = m)
+        rows = lambda: G.gemm(G.OP_N, G.OP_N, r1 - r0, n, k, 1.0, Ar, m, B, k, 0.0, Cr, r1 - r0, N, fast, wr)
+    else:
+        rows = lambda: None
+    out["row_blocks_all_moduli"] = timed(rows)
+    if r1 > r0:
+        del wr, Cr
+    part = torch.empty((2, n, m), dtype=torch.float64, device=A.device)
+    out["fp64_partial_sums_reduce_comm_only"] = timed(lambda: dist.reduce(part, dst=0))
+    del part
+    torch.cuda.empty_cache()
+    flops = 2.0 * m * n * k
+    return {kk: ({"ms_per_step": round(v, 3), "tflops": round(flops / (v * 1e-3) / 1e12, 1)}
+                 if isinstance(v, float) else v) for kk, v in out.items()}
+
+
 def select_workload(args, world):
     """the configuration this run measures: --workload, else cfg2 on one GPU and cfg3 (the moduli-sharded
     BASELINE config) on more; --size / --moduli / --accurate make it a custom one"""
@@ -316,6 +364,9 @@ def main():
                 "kernel": G.last_products_kernel() + " (residue products; int8 ops counted as FLOP, "
                           "2*m'*n'*k' per plane and launch" + (", rank 0's units)" if sharded else ")"),
                 "avg_launch_ms": round(gemm_ms, 4)}
+
+    if sharded and kind == "d" and not args.no_variants:
+        extra["variants"] = time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops)
 
     # accuracy against a double-double reference (testing/eval.hpp semantics); sharded: each rank checks
     # its own output columns, the max is combined

@@ -363,6 +363,54 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
     return C
 
 
+def gemm_moduli_planes_to_root(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
+                               computeType=REAL_DEFAULT, group=None, root=0, ops=None):
+    """SURVEY 8(e) variant (i), kept for comparison with gemm_moduli (bench.py times both): rank r multiplies
+    whole moduli [j0, j1) of moduli_partition (14 over 8 ranks: 2,2,2,2,2,2,1,1) with full shifts of its own,
+    sends each residue plane to the root as soon as it is produced, and the root runs the CRT of all of C.
+    (N - N_root) m n bytes converge on the root; returns C on the root, None elsewhere."""
+    ops = ops or _shard_ops()
+    out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
+    rank, world = _group_info(group)
+    host_sync = dist.get_backend(group) != "nccl"
+    parts = moduli_partition(num_moduli, world)
+    j0, j1 = parts[rank]
+    st = ops.prepare(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, out_dtype, computeType)
+    if j1 > j0 or rank == root:  # every shift on every such rank (a root without moduli needs them for the CRT)
+        ops.stats(st, (0, m), (0, n))
+        if not fastmode:
+            ops.bound(st, (0, n))
+        if j1 > j0:
+            ops.encode(st, j0, j1)
+    groot = _global(group, root)
+    if rank != root:
+        reqs = []
+        for j in range(j0, j1):
+            ops.products(st, j, j + 1, 0, n)
+            if host_sync:
+                ops.sync()
+            reqs += dist.batch_isend_irecv([dist.P2POp(dist.isend, x, groot, group) for x in ops.chunks(st, j, 0, n)])
+        for q in reqs:
+            q.wait()
+        return None
+    rcv = [dist.P2POp(dist.irecv, x, _global(group, r), group)
+           for r, (a, b) in enumerate(parts) if r != root for j in range(a, b) for x in ops.chunks(st, j, 0, n)]
+    side = None if host_sync else ops.side_stream()
+    reqs = []
+    if rcv:
+        if side is not None:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                reqs = dist.batch_isend_irecv(rcv)
+        else:
+            reqs = dist.batch_isend_irecv(rcv)
+    for j in range(j0, j1):
+        ops.products(st, j, j + 1, 0, n)
+    for q in reqs:
+        q.wait()
+    return ops.recombine(st, 0, n)
+
+
 def matmul_moduli(A, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, gather=True, root=0, ops=None,
                   align=TILE):
     """C = A @ B (row-major torch tensors, A, B replicated) sharded over the ranks of `group` (gemm_moduli).

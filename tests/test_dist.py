@@ -120,6 +120,13 @@ def _worker(rank, world, port, case, outdir):
         Cb = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, gather=False, ops=OracleShardOps(),
                               align=16)
         np.save(os.path.join(outdir, f"block{rank}.npy"), Cb.contiguous().numpy())
+        # SURVEY 8(e) variant (i): whole moduli per rank, planes gathered on the root
+        Cp = GD.gemm_moduli_planes_to_root(1, 1, m, n, k, torch.from_numpy(A), k, torch.from_numpy(B), n, N, fast,
+                                           ops=OracleShardOps())
+        if rank == 0:
+            np.save(os.path.join(outdir, "planes.npy"), Cp.t().contiguous().numpy())
+        else:
+            assert Cp is None
         r0, r1 = GD.row_partition(m, world, align=16)[rank]
         Cr = GD.matmul_rows(torch.from_numpy(A[r0:r1].copy()), torch.from_numpy(B), N, fast, gather=True, ops=ops)
         if rank == 0:
@@ -152,7 +159,7 @@ def test_sharded_equals_single_call(tmp_path, world, case):
     A = ((rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))).astype(dt)
     B = ((rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))).astype(dt)
     C = O.gemm(A, B, N, fast)
-    for name in ("moduli", "rows"):
+    for name in ("moduli", "rows", "planes"):
         got = np.load(tmp_path / f"{name}.npy")
         assert got.shape == C.shape
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C).view(np.uint8)), name
