@@ -64,10 +64,10 @@ int gemmul8_gemm_lowmem(void *stream, int op_a, int op_b, size_t m, size_t n, si
 
 /* --- phase entry points (multi-GPU sharding, gemmul8/dist.py) ------------------------------------
  * gemmul8_gemm == gemmul8_split(0, N) + gemmul8_products(0, N) + gemmul8_recombine, on one stream.
- * Splitting the moduli range lets rank r of a modulus-sharded job produce only the residue planes
- * [mod_begin, mod_end) (plane j at work + offR + j * planeR, see gemmul8_layout); the root then
- * receives the other planes into its own workspace and runs gemmul8_recombine.  Every rank
- * computes the full shift vectors (they do not depend on the modulus).
+ * Splitting the moduli range lets a rank produce only the residue planes [mod_begin, mod_end)
+ * (plane j at work + offR + j * planeR, see gemmul8_layout), e.g. to send them to a root that runs
+ * gemmul8_recombine (gemm_moduli_planes_to_root); the sharded entry points further below split the
+ * columns too, and the CRT with them (gemm_moduli).
  *
  * Accurate mode couples the shifts of op(B)'s columns to every row of op(A) (the int8 bound
  * product's column maxima).  A row-block shard therefore runs gemmul8_split_bound, combines the
