@@ -216,8 +216,9 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
     """SURVEY.md 8(e)'s partitions side by side, after the timed region, same operands (a few steps each):
     the default (modulus, column block) units with C gathered on the root; whole moduli per rank with the residue
     planes sent to the root and the root's CRT (variant (i)); row blocks of C, all moduli per rank, no exchange
-    (variant (ii), strong scaling); and the communication alone of the north-star's reduce of FP64 partial CRT
-    sums (two m x n double accumulators to the root; not bit-identical, so not built)."""
+    (variant (ii), strong scaling); its 2-D form (output blocks on a near-square rank grid); and the communication
+    alone of the north-star's reduce of FP64 partial CRT sums (two m x n double accumulators to the root; not
+    bit-identical, so not built)."""
     import torch.distributed as dist
     steps, warm = 3, 1
 
@@ -250,6 +251,21 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
     out["row_blocks_all_moduli"] = timed(rows)
     if r1 > r0:
         del wr, Cr
+    # 2-D output blocks, all moduli per rank (grid R x Q = W with R, Q closest to sqrt(W)): each rank reads and
+    # encodes 1/R of A and 1/Q of B; fast-mode shifts need no exchange, so nothing crosses the fabric
+    R = max(d for d in range(1, int(world ** 0.5) + 1) if world % d == 0)
+    Q = world // R
+    (a0, a1), (b0, b1) = GD.blocks(m, R)[rank // Q], GD.blocks(n, Q)[rank % Q]
+    if fast and a1 > a0 and b1 > b0:
+        wb = G.alloc_work(a1 - a0, b1 - b0, k, N, G.REAL_DEFAULT, A.device)
+        Cb = torch.empty((b1 - b0, a1 - a0), dtype=torch.float64, device=A.device)
+        Ab, Bb = A[:, a0:], B[b0:]
+        blk = lambda: G.gemm(G.OP_N, G.OP_N, a1 - a0, b1 - b0, k, 1.0, Ab, m, Bb, k, 0.0, Cb, a1 - a0, N, fast, wb)
+    else:
+        blk = lambda: None
+    out[f"output_blocks_{R}x{Q}_all_moduli"] = timed(blk)
+    if fast and a1 > a0 and b1 > b0:
+        del wb, Cb
     part = torch.empty((2, n, m), dtype=torch.float64, device=A.device)
     out["fp64_partial_sums_reduce_comm_only"] = timed(lambda: dist.reduce(part, dst=0))
     del part
