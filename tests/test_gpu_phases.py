@@ -397,3 +397,25 @@ def test_moduli_column_shards_randomized():
         got, _ = _simulate_moduli_shards(opA, opB, m, n, k, A, lda, B, ldb, N, fast, out_dtype, ct, world)
         torch.cuda.synchronize()
         assert _same(got, ref), dict(case=case, types=ta + tb, m=m, n=n, k=k, N=N, W=world, fast=fast, op=(opA, opB))
+
+
+def test_output_blocks_fast_mode_same_bits():
+    """fast mode: C blocks of a 2 x 3 rank grid, each from its rows of A and columns of B through plain gemm calls
+    on offset operands (bench.py's output-block variant), assemble to the single call's bits"""
+    import torch
+    import gemmul8 as G
+    from gemmul8 import dist as GD
+    m, n, k, N = 700, 900, 500, 14
+    A = G.randmat(m, k, torch.float64, 0.5, 123456)  # column-major, op N
+    B = G.randmat(k, n, torch.float64, 0.5, 654321)
+    ref = torch.empty((n, m), dtype=torch.float64, device="cuda")
+    G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, ref, m, N, True, G.alloc_work(m, n, k, N))
+    out = torch.full_like(ref, float("nan"))
+    for a0, a1 in GD.blocks(m, 2):
+        for b0, b1 in GD.blocks(n, 3):
+            Cb = torch.empty((b1 - b0, a1 - a0), dtype=torch.float64, device="cuda")
+            G.gemm(G.OP_N, G.OP_N, a1 - a0, b1 - b0, k, 1.0, A[:, a0:], m, B[b0:], k, 0.0, Cb, a1 - a0, N, True,
+                   G.alloc_work(a1 - a0, b1 - b0, k, N))
+            out[b0:b1, a0:a1] = Cb
+    torch.cuda.synchronize()
+    assert _same(out, ref)
