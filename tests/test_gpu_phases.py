@@ -373,9 +373,9 @@ def test_moduli_column_shards_randomized():
     accurate, ops N / T (and C for complex) -- each bit-identical to the single call"""
     import torch
     import gemmul8 as G
-    rng = np.random.default_rng(2027)
+    rng = np.random.default_rng(int(os.environ.get("GEMMUL8_SHARD_FUZZ_SEED", "2027")))
     tdts = {"d": torch.float64, "s": torch.float32, "z": torch.complex128, "c": torch.complex64}
-    for case in range(40):
+    for case in range(int(os.environ.get("GEMMUL8_SHARD_FUZZ_CASES", "40"))):
         ta = tb = "dszc"[int(rng.integers(4))]
         if ta == "d" and rng.random() < 0.3:
             tb = "s"

@@ -191,7 +191,7 @@ def main():
     if len(sys.argv) > 4:  # size ranges: m, n in [a, b), k in [c, d)
         mn, kr = tuple(map(int, sys.argv[3].split(":"))), tuple(map(int, sys.argv[4].split(":")))
     t0 = time.time()
-    out = sweep(cases, seed, mn, kr)
+    out = sweep(cases, seed, mn, kr, ref_epi=os.environ.get("FUZZ_REF_EPI") == "1")
     ran, fails, skipped = out["cases"], out["failures"], out["skipped_defect_classes"]
     unchanged, nonfinite_vec = out["outputs_left_unchanged"], [0] * out["differ_only_in_nonfinite_vectors"]
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
