@@ -82,7 +82,9 @@ int gemmul8_split_bound(void *stream, int op_a, int op_b, size_t m, size_t n, si
                         int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
                         void *work, int compute_type);
 /* flags: GEMMUL8_SPLIT_BOUND_READY (accurate: bound maxima in the workspace, derive the shifts from
- * them), GEMMUL8_SPLIT_SHIFTS_READY (sftA / sftB already in the workspace: encode the slices only) */
+ * them), GEMMUL8_SPLIT_SHIFTS_READY (sftA / sftB already in the workspace: encode the slices only).
+ * mod_begin == mod_end: the shifts only, no slices (e.g. an accurate-mode shard that multiplies no
+ * modulus but recombines columns). */
 int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b, int type_c,
                   const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli, int fastmode, void *work,
                   int compute_type, unsigned mod_begin, unsigned mod_end, int flags);

@@ -331,6 +331,7 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
             operand_shifts(c, v, true, c.st);
             operand_shifts(c, v, false, c.st);
         }
+        if (j1 == j0) return;  // shifts only (a shard that multiplies no modulus but recombines columns)
         const Layout &L = v.L;
         ModParams SP = sub_mod_params(c.N, j0, j1);
         SP.zero_queue = queue_of(v, j0);
@@ -343,9 +344,9 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
     }
     fork(c);
     if (!shifts_ready) operand_shifts(c, v, true, c.st);
-    operand_encode(c, v, true, j0, j1, j0, c.st);
+    if (j1 > j0) operand_encode(c, v, true, j0, j1, j0, c.st);
     if (!shifts_ready) operand_shifts(c, v, false, c.stB);
-    operand_encode(c, v, false, j0, j1, j0, c.stB);
+    if (j1 > j0) operand_encode(c, v, false, j0, j1, j0, c.stB);
     join(c);
 }
 
@@ -595,8 +596,10 @@ int gemmul8_split(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k
     const int rc = oz2::prepare(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, nullptr, A, lda, B, ldb, nullptr,
                                 nullptr, m, num_moduli, fastmode, work, compute_type, c);
     if (rc != GEMMUL8_OK) return rc;
-    if (mod_begin >= mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
+    // mod_begin == mod_end: the shifts only (no slices)
+    if (mod_begin > mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
     if (m == 0 || n == 0) return GEMMUL8_OK;
+    if (mod_begin == mod_end && (flags & GEMMUL8_SPLIT_SHIFTS_READY)) return GEMMUL8_OK;
     oz2::clear_stale_error();
     oz2::LaneGuard lane(c);
     oz2::phase_split(c, oz2::views(work, m, n, k, num_moduli, c.cplx), mod_begin, mod_end,

@@ -203,6 +203,7 @@ class HipShardOps:
         return st["work"][o:o + 4 * (L["bm_pad"] + -(-n // TILE) * TILE)].view(torch.int32)
 
     def encode(self, st, j0, j1):
+        """slices of moduli [j0, j1); accurate mode also derives the final shifts (j0 == j1: only those)"""
         opA, opB, m, n, k, A, lda, B, ldb, N = st["args"]
         fast = st["fast"]
         split(opA, opB, m, n, k, A, lda, B, ldb, N, fast, st["work"], st["dtype"], j0, j1, st["ct"],
@@ -306,9 +307,10 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
         dist.all_reduce(bnd, op=dist.ReduceOp.MAX, group=group)
     mark("shifts")
 
-    # 2. slices of this rank's moduli
+    # 2. slices of this rank's moduli (accurate mode derives the final shifts here too, from sft0 and the bound
+    # maxima: a rank without moduli still needs them for the CRT of its columns)
     j0, j1 = plan.mods[rank]
-    if j1 > j0:
+    if j1 > j0 or not fastmode:
         ops.encode(st, j0, j1)
     mark("encode")
 
@@ -380,7 +382,7 @@ def gemm_moduli_planes_to_root(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14,
         ops.stats(st, (0, m), (0, n))
         if not fastmode:
             ops.bound(st, (0, n))
-        if j1 > j0:
+        if j1 > j0 or not fastmode:  # (accurate: the final shifts even without moduli)
             ops.encode(st, j0, j1)
     groot = _global(group, root)
     if rank != root:

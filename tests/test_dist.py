@@ -72,22 +72,30 @@ class OracleShardOps:
         A8, B8, sA, sB = self.O.scaling(Acm, Bcm, N, fast, opA=opA, opB=opB)
         full = self.O.residues(A8, B8)
         npt = torch.empty((), dtype=out_dtype).numpy().dtype
-        return {"sA": sA, "sB": sB, "full": full, "R": torch.zeros(full.shape, dtype=torch.uint8),
+        # fast mode: the published shifts are what the ranks gather; accurate mode gathers sft0 (stood in for by
+        # the same values here) and derives the final shifts in encode (the native finalize), on every rank
+        return {"sA": sA, "sB": sB, "full": full, "R": torch.zeros(full.shape, dtype=torch.uint8), "fast": fast,
                 "pA": torch.full((m,), self.SENTINEL, dtype=torch.int16),
-                "pB": torch.full((n,), self.SENTINEL, dtype=torch.int16), "dtype": npt}
+                "pB": torch.full((n,), self.SENTINEL, dtype=torch.int16),
+                "gA": torch.full((m,), self.SENTINEL, dtype=torch.int16),
+                "gB": torch.full((n,), self.SENTINEL, dtype=torch.int16), "dtype": npt}
 
     def stats(self, st, rows, cols):
-        st["pA"][rows[0]:rows[1]] = torch.from_numpy(st["sA"][rows[0]:rows[1]])
-        st["pB"][cols[0]:cols[1]] = torch.from_numpy(st["sB"][cols[0]:cols[1]])
+        a, b = (st["pA"], st["pB"]) if st["fast"] else (st["gA"], st["gB"])
+        a[rows[0]:rows[1]] = torch.from_numpy(st["sA"][rows[0]:rows[1]])
+        b[cols[0]:cols[1]] = torch.from_numpy(st["sB"][cols[0]:cols[1]])
 
     def shift_vectors(self, st):
-        return st["pA"], st["pB"]
+        return (st["pA"], st["pB"]) if st["fast"] else (st["gA"], st["gB"])
 
     def bound(self, st, cols):
         return torch.zeros(8, dtype=torch.int32)  # (the oracle derives accurate shifts itself)
 
     def encode(self, st, j0, j1):
-        pass
+        if not st["fast"]:  # the final shifts, from the assembled sft0 (complete only after the gathers)
+            assert int(st["gA"].min()) != self.SENTINEL or st["gA"].numel() == 0
+            st["pA"][:] = torch.from_numpy(st["sA"])
+            st["pB"][:] = torch.from_numpy(st["sB"])
 
     def products(self, st, j0, j1, c0, c1):
         st["R"][j0:j1, c0:c1] = torch.from_numpy(st["full"][j0:j1, c0:c1])
@@ -149,6 +157,7 @@ def _worker(rank, world, port, case, outdir):
     (2, (40, 50, 60, 6, True, np.complex128)),
     (8, (120, 300, 64, 14, True, np.float64)),  # the cfg3 plan: 14 moduli, 8 ranks, 7 units each
     (8, (60, 130, 40, 9, False, np.float64)),
+    (7, (90, 45, 50, 3, False, np.float64)),   # accurate: rank 1 multiplies no modulus but owns columns
 ])
 def test_sharded_equals_single_call(tmp_path, world, case):
     sys.path.insert(0, ROOT)
