@@ -181,7 +181,7 @@ def _simulate_moduli_shards(opA, opB, m, n, k, A, lda, B, ldb, N, fast, out_dtyp
             st[r]["work"][L["offBound"]:L["offBound"] + 4 * comb.numel()].view(torch.int32).copy_(comb)
     for r in range(world):
         j0, j1 = plan.mods[r]
-        if j1 > j0:
+        if j1 > j0 or not fast:  # (accurate: the final shifts even without moduli)
             ops[r].encode(st[r], j0, j1)
     for t in range(plan.stages):
         for r in range(world):

@@ -65,7 +65,7 @@ def main():
             st[r]["work"][L["offBound"]:L["offBound"] + 4 * comb.numel()].view(torch.int32).copy_(comb)
     for r in range(W):
         j0, j1 = plan.mods[r]
-        if j1 > j0:
+        if j1 > j0 or not fast:
             ops[r].encode(st[r], j0, j1)
     torch.cuda.synchronize()
     for r in range(W):
