@@ -358,9 +358,10 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
         return None
     C = torch.empty((n, m), dtype=out_dtype, device=Cb.device)
     C[c0:c1] = Cb
-    rq = [dist.irecv(C[s0:s1], src=_global(group, s), group=group)
+    # one group: the blocks arrive concurrently, each over its sender's own link
+    rq = [dist.P2POp(dist.irecv, C[s0:s1], _global(group, s), group)
           for s, (s0, s1) in enumerate(plan.cols) if s != root and s1 > s0]
-    for q in rq:
+    for q in (dist.batch_isend_irecv(rq) if rq else []):
         q.wait()
     return C
 
