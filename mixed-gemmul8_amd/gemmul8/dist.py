@@ -509,17 +509,19 @@ def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=
     ops.sync()
     groot = _global(group, root)
     if rank != root:
-        dist.send(C_local.contiguous(), dst=groot, group=group)
+        if C_local.shape[0]:
+            dist.send(C_local.contiguous(), dst=groot, group=group)
         return None
     parts = []
-    reqs = []
+    ops_ = []
     for r in range(world):
         if r == root:
             parts.append(C_local)
             continue
         buf = torch.empty((sizes[r], C_local.shape[1]), dtype=C_local.dtype, device=C_local.device)
-        reqs.append(dist.irecv(buf, src=_global(group, r), group=group))
+        if sizes[r]:
+            ops_.append(dist.P2POp(dist.irecv, buf, _global(group, r), group))
         parts.append(buf)
-    for q in reqs:
+    for q in (dist.batch_isend_irecv(ops_) if ops_ else []):  # concurrent, one link per sender
         q.wait()
     return torch.cat(parts, 0)
