@@ -155,7 +155,9 @@ def cpu_baseline(size_hint, dev):
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     threads = O.num_threads()
-    n = size_hint or 5120  # about 14 s of the oracle on 16 host threads (6.9 s at 4096)
+    # the full cfg2 size (full size when it fits the time budget): the oracle's int8 products run
+    # blocked on AVX-512 VNNI where the host has it (about 4 s at 4096 on 8 threads of this container)
+    n = size_hint or 8192
     A = G.randmat(n, n, torch.float64, 0.5, 123456, dev).cpu().numpy().T  # column-major n x n (F order)
     t0 = time.perf_counter()
     C = O.gemm(A, A, 14, True)
@@ -165,8 +167,8 @@ def cpu_baseline(size_hint, dev):
     out = {"value": 2.0 * n ** 3 / dt / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
            "sample": f"cfg2 workload at m=n=k={n} (DGEMM emulation, num_moduli=14, fast mode, reference "
                      f"generator seed 123456, A == B), one call ({dt:.1f} s) of the oracle/oz2_oracle.c "
-                     f"restatement with {threads} OpenMP threads on {_cpu_model()} ({os.cpu_count()} logical "
-                     f"CPUs visible)",
+                     f"restatement (int8 products on AVX-512 VNNI: {O.vnni()}) with {threads} OpenMP threads on "
+                     f"{_cpu_model()} ({os.cpu_count()} logical CPUs visible)",
            "relerr_max_vs_fp64": float(rel.max()), "relerr_median_vs_fp64": float(np.median(rel))}
     # cfg1 in full: SGEMM emulation 1024^3, N = 4, fast mode (BASELINE.json configs[0])
     A1 = G.randmat(1024, 1024, torch.float32, 0.5, 123456, dev).cpu().numpy().T

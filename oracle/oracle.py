@@ -32,6 +32,8 @@ def lib():
         _lib.oz2o_residues.argtypes = [sz, sz, sz, u, p, p, p]
         _lib.oz2o_crt.argtypes = [c, i, sz, sz, u, p, p, p, p, p, p, sz, i]
         _lib.oz2o_gemm.argtypes = [c, c, c, i, i, sz, sz, sz, p, p, sz, p, sz, p, p, sz, u, i, i, i, p, p, i]
+        _lib.oz2o_vnni.restype = i
+        _lib.oz2o_vnni.argtypes = []
     return _lib
 
 
@@ -125,3 +127,8 @@ def gemm(A, B, num_moduli, fastmode=True, out_dtype=None, alpha=1.0, beta=0.0, C
 
 def num_threads():
     return lib().oz2o_num_threads()
+
+
+def vnni():
+    """whether the int8 products take the AVX-512 VNNI path (exact either way; OZ2O_SCALAR=1 forces scalar)"""
+    return bool(lib().oz2o_vnni())
