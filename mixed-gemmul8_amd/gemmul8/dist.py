@@ -44,6 +44,7 @@ a CPU implementation to exercise the communication pattern under gloo.  Workspac
 shape on the ops object (one object serves one call at a time), so repeated calls allocate only
 their output.
 """
+import functools
 import math
 
 import torch
@@ -147,6 +148,11 @@ class ShardPlan:
             if q != r:
                 out += [(q, j, a, b) for (s, j, a, b) in self.sends(q, t) if s == r]
         return out
+
+
+@functools.lru_cache(maxsize=64)
+def _plan(m, n, num_moduli, world, align):
+    return ShardPlan(m, n, num_moduli, world, align)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -279,7 +285,7 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
     ops = ops or _shard_ops()
     out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
     rank, world = _group_info(group)
-    plan = ShardPlan(m, n, num_moduli, world, align)  # (align: the native products need TILE)
+    plan = _plan(m, n, num_moduli, world, align)  # (align: the native products need TILE)
     # the gloo backend reads device tensors without waiting on the compute stream
     host_sync = dist.get_backend(group) != "nccl"
     st = ops.prepare(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, out_dtype, computeType)
