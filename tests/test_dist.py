@@ -158,6 +158,7 @@ def _worker(rank, world, port, case, outdir):
     (8, (120, 300, 64, 14, True, np.float64)),  # the cfg3 plan: 14 moduli, 8 ranks, 7 units each
     (8, (60, 130, 40, 9, False, np.float64)),
     (7, (90, 45, 50, 3, False, np.float64)),   # accurate: rank 1 multiplies no modulus but owns columns
+    (3, (40, 50, 61, 7, False, np.complex128)),
 ])
 def test_sharded_equals_single_call(tmp_path, world, case):
     sys.path.insert(0, ROOT)
