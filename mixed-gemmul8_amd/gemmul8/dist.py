@@ -259,18 +259,28 @@ def _global(group, r):
     return dist.get_global_rank(group, r) if group is not None else r
 
 
-def _allgather_blocks(vec, blks, rank, group):
-    """vec[b0:b1] of every rank's block (blocks(len, W) layout) assembled into every rank's vec"""
-    chunk = blks[0][1] - blks[0][0]
-    if chunk == 0:
+def _allgather_blocks(vecs, blks, rank, group):
+    """vec[b0:b1] of every rank's block (blocks(len, W) layout) assembled into every rank's vec, for each
+    (vec, blks) pair of the lists -- one all-gather for all of them"""
+    chunks = [b[0][1] - b[0][0] for b in blks]
+    total = sum(chunks)
+    if total == 0:
         return
-    b0, b1 = blks[rank]
-    mine = vec.new_zeros(chunk)
-    mine[:b1 - b0] = vec[b0:b1]
-    parts = [vec.new_empty(chunk) for _ in blks]
+    mine = vecs[0].new_zeros(total)
+    o = 0
+    for vec, b, ch in zip(vecs, blks, chunks):
+        b0, b1 = b[rank]
+        mine[o:o + b1 - b0] = vec[b0:b1]
+        o += ch
+    parts = [mine.new_empty(total) for _ in blks[0]]
     # moved as bytes: RCCL has no 16-bit integer type
     dist.all_gather([p.view(torch.uint8) for p in parts], mine.view(torch.uint8), group=group)
-    vec.copy_(torch.cat(parts)[:vec.numel()])
+    allp = torch.stack(parts)  # [rank][total]
+    o = 0
+    for vec, ch in zip(vecs, chunks):
+        if ch:
+            vec.copy_(allp[:, o:o + ch].reshape(-1)[:vec.numel()])
+        o += ch
 
 
 def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
@@ -304,8 +314,7 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
     if host_sync:
         ops.sync()
     va, vb = ops.shift_vectors(st)
-    _allgather_blocks(va, plan.rows, rank, group)
-    _allgather_blocks(vb, plan.cols, rank, group)
+    _allgather_blocks([va, vb], [plan.rows, plan.cols], rank, group)
     if not fastmode:
         bnd = ops.bound(st, plan.cols[rank])
         if host_sync:
