@@ -259,6 +259,14 @@ def _global(group, r):
     return dist.get_global_rank(group, r) if group is not None else r
 
 
+def _send(t, dst, group):
+    """one send posted as a batched P2P op: RCCL matches it against the receiver's batched irecv on the
+    group's own communicator whether or not the group was initialised eagerly (a plain dist.send on a lazily
+    initialised NCCL group goes over a separate two-rank communicator and never meets a batched receive)"""
+    for q in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, dst, group)]):
+        q.wait()
+
+
 def _allgather_blocks(vecs, blks, rank, group):
     """vec[b0:b1] of every rank's block (blocks(len, W) layout) assembled into every rank's vec, for each
     (vec, blks) pair of the lists -- one all-gather for all of them"""
@@ -369,7 +377,7 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
         ops.sync()
     if rank != root:
         if c1 > c0:
-            dist.send(Cb.contiguous(), dst=_global(group, root), group=group)
+            _send(Cb.contiguous(), _global(group, root), group)
         return None
     C = torch.empty((n, m), dtype=out_dtype, device=Cb.device)
     C[c0:c1] = Cb
@@ -525,7 +533,7 @@ def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=
     groot = _global(group, root)
     if rank != root:
         if C_local.shape[0]:
-            dist.send(C_local.contiguous(), dst=groot, group=group)
+            _send(C_local.contiguous(), groot, group)
         return None
     parts = []
     ops_ = []
