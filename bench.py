@@ -410,6 +410,14 @@ def main():
             extra["relerr_max"] = emax
             extra["relerr_median"] = emed
             del C1, C2
+            # a second, independent seed pair (A 123456, B 654321) beside the reference's A == B
+            B2 = G.randmat(k, n, torch.float64, 0.5, 654321, dev)
+            C2o = torch.empty((n, m), dtype=tc, device=dev)
+            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B2, k, 0.0, C2o, m, N, fast, work, ct)
+            C1, C2 = G.dd_gemm(A, B2, m, n, k)
+            emax2, emed2 = G.relerr_dd(C2o, C1, C2)
+            extra["relerr_seed_pair_123456_654321"] = {"max": emax2, "median": emed2}
+            del C1, C2, B2, C2o
 
     if rank == 0:
         # measured live after the timed region: the same MFMA alone on uniformly random operand bytes
