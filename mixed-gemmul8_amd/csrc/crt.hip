@@ -216,6 +216,60 @@ __device__ __forceinline__ void kara_dword(uint32_t x1, uint32_t x2, uint32_t x3
     re = rE | (rO << 8);
     im = tE | (tO << 8);
 }
+// The same residues in two steps, so that only two sub-planes' words are live at a time: from P1 and P2,
+// Re = (b1 - b2) mod p and S = (b1 + b2) mod p (b1 + b2 < 2p, so (e, e - p) holds exactly one value below p);
+// later Im = (b3 - S) mod p, which equals (b3 - b1 - b2) mod p.
+template <int P>
+__device__ __forceinline__ void kara_pair_dword(uint32_t x1, uint32_t x2, uint32_t &re, uint32_t &sum) {
+    const u16x2 p1 = {(unsigned short)P, (unsigned short)P};
+    auto lanes = [&](uint32_t a1, uint32_t a2, uint32_t &r, uint32_t &t) {
+        const u16x2 e1 = __builtin_bit_cast(u16x2, a1), e2 = __builtin_bit_cast(u16x2, a2);
+        const u16x2 d = e1 - e2, e = e1 + e2;
+        r = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(d, d + p1));
+        t = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(e, e - p1));
+    };
+    constexpr uint32_t LO = 0x00ff00ffu;
+    uint32_t rE, tE, rO, tO;
+    lanes(x1 & LO, x2 & LO, rE, tE);
+    lanes((x1 >> 8) & LO, (x2 >> 8) & LO, rO, tO);
+    re = rE | (rO << 8);
+    sum = tE | (tO << 8);
+}
+template <int P> __device__ __forceinline__ uint32_t kara_sub_dword(uint32_t x3, uint32_t sum) {
+    const u16x2 p1 = {(unsigned short)P, (unsigned short)P};
+    auto lanes = [&](uint32_t a3, uint32_t s) {
+        const u16x2 d = __builtin_bit_cast(u16x2, a3) - __builtin_bit_cast(u16x2, s);
+        return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(d, d + p1));
+    };
+    constexpr uint32_t LO = 0x00ff00ffu;
+    return lanes(x3 & LO, sum & LO) | (lanes((x3 >> 8) & LO, (sum >> 8) & LO) << 8);
+}
+template <unsigned N, unsigned... I>
+__device__ __forceinline__ void kara_pair_words(const uint64_t (&w1)[N], const uint64_t (&w2)[N], uint64_t (&re)[N],
+                                                uint64_t (&sum)[N], std::integer_sequence<unsigned, I...>) {
+    auto one = [&](auto ic) {
+        constexpr unsigned i = decltype(ic)::value;
+        uint32_t r0, s0, r1, s1;
+        kara_pair_dword<oz2_p[i]>((uint32_t)w1[i], (uint32_t)w2[i], r0, s0);
+        kara_pair_dword<oz2_p[i]>((uint32_t)(w1[i] >> 32), (uint32_t)(w2[i] >> 32), r1, s1);
+        re[i] = (uint64_t)r0 | ((uint64_t)r1 << 32);
+        sum[i] = (uint64_t)s0 | ((uint64_t)s1 << 32);
+        asm volatile("" : "+v"(re[i]), "+v"(sum[i]));  // computed here, so P1's and P2's words die here
+    };
+    (one(std::integral_constant<unsigned, I>{}), ...);
+}
+template <unsigned N, unsigned... I>
+__device__ __forceinline__ void kara_sub_words(const uint64_t (&w3)[N], uint64_t (&sum_im)[N],
+                                               std::integer_sequence<unsigned, I...>) {
+    auto one = [&](auto ic) {
+        constexpr unsigned i = decltype(ic)::value;
+        const uint32_t lo = kara_sub_dword<oz2_p[i]>((uint32_t)w3[i], (uint32_t)sum_im[i]);
+        const uint32_t hi = kara_sub_dword<oz2_p[i]>((uint32_t)(w3[i] >> 32), (uint32_t)(sum_im[i] >> 32));
+        sum_im[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        asm volatile("" : "+v"(sum_im[i]));
+    };
+    (one(std::integral_constant<unsigned, I>{}), ...);
+}
 template <unsigned N, unsigned... I>
 __device__ __forceinline__ void kara_words(const uint64_t (&w1)[N], const uint64_t (&w2)[N], const uint64_t (&w3)[N],
                                            uint64_t (&re)[N], uint64_t (&im)[N], std::integer_sequence<unsigned, I...>) {
@@ -269,17 +323,46 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
             uint64_t w[N], wi[N];
             const size_t off = col * a.ldr + r0;
             if constexpr (KARA) {
-                uint64_t w1[N], w2[N], w3[N];
+                // real parts from P1, P2 first, then the imaginary parts with P3: two sub-planes' words
+                // live at a time instead of three (occupancy; the residues are the same bytes)
+                uint64_t w1[N], w2[N];
                 load_rows<N>(a, off, nr == CRT_ROWS, nr, w1);
                 load_rows<N>(a, off + a.sub, nr == CRT_ROWS, nr, w2);
-                load_rows<N>(a, off + 2 * a.sub, nr == CRT_ROWS, nr, w3);
-                kara_words<N>(w1, w2, w3, w, wi, std::make_integer_sequence<unsigned, N>{});
+                kara_pair_words<N>(w1, w2, w, wi, std::make_integer_sequence<unsigned, N>{});
+                // P3's loads go out after that (an opaque dependency on the last combined word keeps the
+                // compiler from merging them with P1's and P2's), in flight under the real parts
+                size_t off3 = off + 2 * a.sub;
+                asm volatile("" : "+v"(off3) : "v"(wi[N - 1]));
+                uint64_t w3[N];
+                load_rows<N>(a, off3, nr == CRT_ROWS, nr, w3);
+#pragma unroll
+                for (int e = 0; e < CRT_ROWS; ++e) {
+                    uint8_t r[N];
+#pragma unroll
+                    for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
+                    const double vr = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}),
+                                             (int)sa[e] + sB);
+                    if constexpr (OT == 2) wb[crt_slot<E>(lane, e)].x = vr;
+                    else wb[crt_slot<E>(lane, e)].x = __double2float_rn(vr);
+                }
+                asm volatile("" ::: "memory");  // the real parts go to LDS now (no merging with the imaginary ones)
+                kara_sub_words<N>(w3, wi, std::make_integer_sequence<unsigned, N>{});
+#pragma unroll
+                for (int e = 0; e < CRT_ROWS; ++e) {
+                    uint8_t r[N];
+#pragma unroll
+                    for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(wi[i] >> (8 * e));
+                    const double vi = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}),
+                                             (int)sa[e] + sB);
+                    if constexpr (OT == 2) wb[crt_slot<E>(lane, e)].y = vi;
+                    else wb[crt_slot<E>(lane, e)].y = __double2float_rn(vi);
+                }
             } else {
                 load_rows<N>(a, off, nr == CRT_ROWS, nr, w);
                 if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == CRT_ROWS && (a.imag_off & 7) == 0, nr, wi);
             }
 #pragma unroll
-            for (int e = 0; e < CRT_ROWS; ++e) {
+            for (int e = 0; e < (KARA ? 0 : CRT_ROWS); ++e) {
                 uint8_t r[N];
 #pragma unroll
                 for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
