@@ -1,0 +1,51 @@
+"""Register / LDS budgets of the hot gfx950 kernels, read from the built library's code-object metadata
+(tools/kernel_resources.py; no GPU needed).  A source change elsewhere in a kernel can push it across an
+occupancy step without any visible sign: in round 3 the reference-epilogue code took the Karatsuba CRT from
+164 to 172 VGPRs, 3 -> 2 waves per SIMD, and cfg5's CRT from 0.202 to 0.231 ms.  The floors below are the
+occupancies the measured timings in DESIGN.md were taken at."""
+import os
+import shutil
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+pytestmark = pytest.mark.skipif(not shutil.which("llvm-readelf", path="/opt/rocm/llvm/bin"),
+                                reason="ROCm LLVM tools absent")
+
+# demangled-name prefix -> minimum waves per SIMD
+FLOORS = {
+    "oz2::gemm_i8_persistent_kernel<false, 1, 0>": 2,  # cfg2/3/4 products: 512 threads, 160 KiB LDS, 1 block per CU
+    "oz2::gemm_i8_persistent_kernel<true, 1, 0>": 2,   # cfg5 (Karatsuba sub-products)
+    "oz2::crt_kernel<0, false, 14u, false>": 5,        # cfg2/3 CRT
+    "oz2::crt_kernel<0, false, 10u, false>": 5,        # cfg4 CRT
+    "oz2::crt_kernel<2, false, 12u, true>": 3,         # cfg5 CRT (Karatsuba residues)
+    "oz2::stats_pair_kernel<16, true>": 8,             # cfg2 shifts
+    "oz2::encode_pair_kernel<double, false, false, true, true>": 4,  # cfg2 slices
+    "oz2::encode_kernel<double, true, false, false, 0, true>": 2,    # cfg5 slices
+}
+
+
+@pytest.fixture(scope="module")
+def table():
+    import kernel_resources as K
+    lib = K.LIB
+    assert os.path.exists(lib), "build first: make -C mixed-gemmul8_amd"
+    res = K.resources(lib)
+    dm = K.demangled(sorted(res))
+    return {dm[n]: v for n, v in res.items()}
+
+
+def test_no_kernel_uses_scratch(table):
+    bad = {n: v["scratch"] for n, v in table.items() if v["scratch"] or v["vgpr_spill"]}
+    assert not bad, bad
+
+
+@pytest.mark.parametrize("prefix", sorted(FLOORS))
+def test_hot_kernel_occupancy(table, prefix):
+    hits = {n: v for n, v in table.items() if n.startswith("void " + prefix + "(")}
+    assert hits, f"{prefix} not in the library"
+    for n, v in hits.items():
+        assert v["occupancy"] >= FLOORS[prefix], (n, v)
