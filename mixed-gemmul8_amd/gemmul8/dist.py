@@ -53,6 +53,10 @@ import torch.distributed as dist
 from . import (OP_N, OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, gemm, layout, split, split_bound,
                products, recombine, shard_stats, shard_bound)
 
+__all__ = ["OP_N", "OP_T", "REAL_DEFAULT", "COMPLEX_BIG_MATRIX_ENCODE", "ShardPlan", "HipShardOps", "HipOps", "blocks",
+           "moduli_partition", "row_partition", "gemm_moduli", "gemm_moduli_planes_to_root", "matmul_moduli",
+           "matmul_rows"]
+
 TILE = 256  # product tile edge: column blocks of the product units start at multiples of it
 
 
