@@ -390,6 +390,9 @@ __global__ __launch_bounds__(256) void stats_pair_kernel(const double *__restric
 // pass 2: encode.  Tile = 64 vectors x KT elements through LDS.
 //   MODE 0: residues of trunc(x * 2^sft), N planes (fast & accurate modes)
 //   MODE 1: 6-bit magnitudes ceil(|x| * 2^sft0), 1 plane (accurate-mode bound)
+//   MODE 2: MODE 0 for f32 operands whose residues need mod_8i<float>'s four f32 steps (N > 10), in a
+//           kernel without the f64 group form, whose registers (260 for complex f32) would otherwise set
+//           its occupancy
 // Complex A (IS_A): row v <- [re, -im], row v+m <- [im, re]  (scaling.hpp:753-838)
 // Complex B:        col v <- [re; im]                           (scaling.hpp:1150-1230)
 // flags: ENC_CONJ (op C: the imaginary part enters negated, scaling.hpp:840-1089,
@@ -617,28 +620,16 @@ __device__ __forceinline__ void encode_vec16(const R (&yr)[16], const R (&yi)[16
         }
     };
 
-    if constexpr (std::is_same<R, double>::value) {
-        residues_f64(yr, yi);
-    } else if (G.f32_exact) {
-        // f32 operands whose residues mod_8i<float> computes exactly (G.f32_exact): the same
-        // residues through the f64 group form, a fraction of the f32 work
-        double dr[16], di[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q) {
-            dr[q] = (double)yr[q];
-            di[q] = CPLX ? (double)yi[q] : 0.0;
-        }
-        residues_f64(dr, di);
-    } else {
-        // f32 operands, any N: mod_8i's four f32 steps per modulus (scaling.hpp:225-230)
+    // f32 operands, any N: mod_8i's four f32 steps per modulus (scaling.hpp:225-230)
+    auto f32_steps = [&]() {
         for (unsigned j = 0; j < MP.N; ++j) {
             const int p = MP.p[j];
             const float rf = MP.rinv_f[j];
             int rr[16], ri[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                rr[q] = mod8_f32(yr[q], p, rf);
-                ri[q] = CPLX ? mod8_f32(yi[q], p, rf) : 0;
+                rr[q] = mod8_f32((float)yr[q], p, rf);
+                ri[q] = CPLX ? mod8_f32((float)yi[q], p, rf) : 0;
             }
             uint32_t wr[4], wi[4];
 #pragma unroll
@@ -656,6 +647,24 @@ __device__ __forceinline__ void encode_vec16(const R (&yr)[16], const R (&yi)[16
             if (kara) sum_words(rr, ri, p, ws);
             emit(out + (size_t)j * plane, wr, wi, ws);
         }
+    };
+
+    if constexpr (std::is_same<R, double>::value) {
+        residues_f64(yr, yi);
+    } else if constexpr (MODE == 2) {
+        f32_steps();
+    } else if (G.f32_exact) {
+        // f32 operands whose residues mod_8i<float> computes exactly (G.f32_exact): the same
+        // residues through the f64 group form, a fraction of the f32 work
+        double dr[16], di[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            dr[q] = (double)yr[q];
+            di[q] = CPLX ? (double)yi[q] : 0.0;
+        }
+        residues_f64(dr, di);
+    } else {
+        f32_steps();
     }
 }
 
@@ -723,14 +732,14 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
     const size_t v = v0 + vl;
     const size_t kk = e0 + 16 * c;
     int s = 0;
-    if (v < nvec) s = MODE == 0 ? -(int)sft[v] : sft0_scale<R>(sft[v]);
+    if (v < nvec) s = MODE != 1 ? -(int)sft[v] : sft0_scale<R>(sft[v]);
 
     R yr[16], yi[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
         R re = tile[16 * c + q][vl][0];
         R im = CPLX ? tile[16 * c + q][vl][NC - 1] : R(0);
-        if (MODE == 0) {
+        if (MODE != 1) {
             yr[q] = trunc(scalbn(re, s));
             yi[q] = trunc(scalbn(im, s));
         } else {
@@ -864,10 +873,16 @@ static void launch_encode(const void *X, size_t ld, bool contig, size_t nvec, si
                          : dim3((unsigned)(vpad_grid / 64), (unsigned)(L.kblk / KT));
     const ModGroups G = make_groups(MP, L.N);  // grouping by the call's N (magnitude bound), not the sub-range
     const bool nt = nvec * len * sizeof(R) * (CPLX ? 2 : 1) >= NT_OPERAND_BYTES;
+// MODE 2 exists for f32 operands only
+#define OZ2_EN_F32(cg) do { if constexpr (std::is_same<R, float>::value) OZ2_EN(cg, 2); } while (0)
 #define OZ2_EN(cg, md) do { if (nt) launch(encode_kernel<R, CPLX, cg, IS_A, md, true>, grid, dim3(NT), st, x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G); \
                             else launch(encode_kernel<R, CPLX, cg, IS_A, md, false>, grid, dim3(NT), st, x, ld, nvec, len, sft, out, plane, L.ksteps, L.kblk, vmax, flags, MP, G); } while (0)
-    if (contig) { if (mode == 0) OZ2_EN(true, 0); else OZ2_EN(true, 1); }
-    else { if (mode == 0) OZ2_EN(false, 0); else OZ2_EN(false, 1); }
+    if constexpr (std::is_same<R, float>::value) {
+        if (mode == 0 && !G.f32_exact) mode = 2;
+    }
+    if (contig) { if (mode == 0) OZ2_EN(true, 0); else if (mode == 1) OZ2_EN(true, 1); else OZ2_EN_F32(true); }
+    else { if (mode == 0) OZ2_EN(false, 0); else if (mode == 1) OZ2_EN(false, 1); else OZ2_EN_F32(false); }
+#undef OZ2_EN_F32
 #undef OZ2_EN
 }
 
