@@ -512,6 +512,22 @@ def test_encode_form_boundaries(N, fast, dt):
     check_full(A, B, N, fast=fast)
 
 
+@pytest.mark.parametrize("N", [11, 14, 20])
+@pytest.mark.parametrize("types", ["dsd", "sds", "zcz", "czc"])
+def test_f32_four_step_encode_instantiation(N, types):
+    """f32 operands above N = 10 in their own encode launch (operand types differ, so no pair kernel):
+    the four-step-only instantiation (split.hip MODE 2), slices and output bit for bit against the oracle,
+    with the same wide dynamic range as the form-boundary test"""
+    ta, tb, tc = types
+    rng = np.random.default_rng(1300 + N + 7 * ord(ta))
+    m, n, k = 140, 110, 260
+    A = randmat_np(rng, m, k, phi=3.0, dtype=_NPT[ta])
+    B = randmat_np(rng, k, n, phi=3.0, dtype=_NPT[tb])
+    if N > 19 and ta in "cz":
+        N = 19  # complex fast mode with 20 moduli is a reference defect (DESIGN.md section 10.6)
+    check_full(A, B, N, fast=True, out_dtype=_NPT[tc])
+
+
 @pytest.mark.parametrize("fast", [True, False])
 def test_offset_pointers(fast):
     """A, B and C one element past an allocation's start (8-byte aligned only) and the workspace 16
