@@ -109,12 +109,21 @@ def dist_setup():
         backend = os.environ.get("GEMMUL8_BENCH_BACKEND", "nccl")
         local = local % max(torch.cuda.device_count(), 1)
         torch.cuda.set_device(local)
+        # stdout carries rank 0's one JSON line only: what the communication libraries print while they
+        # connect (gloo announces its peers on fd 1) goes to stderr, and so does everything of the other ranks
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        dist.barrier()  # the connections are up before stdout is given back
         world = dist.get_world_size()
         rank = dist.get_rank()
+        if rank == 0:
+            os.dup2(saved, 1)
+        os.close(saved)
     else:
         torch.cuda.set_device(0)
     return world, rank, backend
