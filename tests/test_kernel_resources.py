@@ -38,6 +38,18 @@ def table():
     return {dm[n]: v for n, v in res.items()}
 
 
+def test_occupancy_formula():
+    """waves per SIMD: 512 registers per lane in granules of 8, 160 KiB of LDS per CU over 4 SIMDs, at most 8"""
+    import kernel_resources as K
+    assert K.occupancy(81, 0, 16384, 256) == 5      # the real CRT: 88 registers -> 5
+    assert K.occupancy(156, 0, 32768, 256) == 3     # the Karatsuba CRT
+    assert K.occupancy(172, 0, 32768, 256) == 2     # ... as it had drifted
+    assert K.occupancy(238, 0, 163840, 512) == 2    # the product kernel: one 512-thread block per CU
+    assert K.occupancy(62, 0, 19328, 256) == 8      # the stats pair kernel
+    assert K.occupancy(260, 4, 16640, 128) == 1     # 264 registers: one wave
+    assert K.occupancy(102, 0, 16640, 128) == 4     # 128-thread blocks: LDS allows 9 blocks = 18 waves / 4
+
+
 def test_no_kernel_uses_scratch(table):
     bad = {n: v["scratch"] for n, v in table.items() if v["scratch"] or v["vgpr_spill"]}
     assert not bad, bad
