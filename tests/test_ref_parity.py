@@ -4,7 +4,6 @@ BASELINE size (cfg2: 8192^3, 14 moduli).  Expectation: C bit-identical.
 
 Also records both implementations' wall time per call into gpurun_out/ref_compare.json
 (the reference's own 4 phase timers include its device-wide syncs)."""
-import ctypes
 import json
 import os
 import sys
@@ -16,22 +15,10 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-REF = os.path.join(ROOT, "oracle", "_ref", "libgemmul8_ref.so")
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from ref_sweep import CODES, _extreme, _ref, sweep  # noqa: E402
+
 RESULTS = {}
-
-
-def _ref():
-    if not os.path.exists(REF):
-        pytest.skip("oracle/_ref not built (needs /root/reference at build time)")
-    lib = ctypes.CDLL(REF)
-    p, sz, i, u = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint
-    lib.ref_gemm.argtypes = [i, i, i, i, i, sz, sz, sz, p, p, sz, p, sz, p, p, sz, u, i, i, p, p]
-    lib.ref_work_size.restype = sz
-    lib.ref_work_size.argtypes = [sz, sz, sz, u, i]
-    return lib
-
-
-CODES = {"d": 0, "s": 1, "z": 2, "c": 3}
 
 
 # (ta, tb, tc, m, n, k, num_moduli, fast, opA, opB, computeType)
@@ -105,26 +92,6 @@ def test_same_inputs_same_bits(case):
     with open(os.path.join(ROOT, "gpurun_out", "ref_compare.json"), "w") as f:
         json.dump(RESULTS, f, indent=1)
     assert same and nbad == 0, f"{nbad} elements differ from the reference"
-
-
-def _extreme(X, vec_axis, big, tiny, sub):
-    """Vectors of a column-major matrix held as a torch tensor overwritten with extreme magnitudes
-    (vec_axis 1: the rows of A, X[e, v]; 0: the columns of B, X[v, e]): vector 0 subnormal, 1 alternating big / tiny, 2 a single subnormal element, 3 zero, 4 big (its
-    sum of squares overflows), 5 negative zeros and one normal element."""
-    import torch
-    V = X if vec_axis == 1 else X.t()  # V[e, v]: element e of vector v
-    V[:, 0] *= sub
-    alt = torch.ones(V.shape[0], dtype=V.real.dtype if V.is_complex() else V.dtype, device=V.device)
-    alt[0::2] = big
-    alt[1::2] = tiny
-    V[:, 1] *= alt
-    V[:, 2] = 0
-    V[V.shape[0] // 2, 2] = sub
-    V[:, 3] = 0
-    V[:, 4] *= big
-    V[:, 5] = -0.0
-    V[1, 5] = 0.75
-    return X
 
 
 # (ta, tb, tc, m, n, k, num_moduli, fast, computeType)
@@ -259,14 +226,12 @@ def test_complex_alpha_beta_same_bits(case):
     dict(seed=104, extreme=True, ab_mode="general", ld=False, ref_epi=True),
 ])
 def test_randomized_live_parity(mode):
-    """tools/probes/fuzz_ref.py as a test: 300 random calls (the 12 type combinations, N = 2..20, both modes,
+    """tests/ref_sweep.py: 300 random calls (the 12 type combinations, N = 2..20, both modes,
     ops N/T/C, the three complex compute types, general and complex alpha / beta; padded leading dimensions;
     extreme and non-finite inputs) through both builds, C compared byte for byte.  Skipped: the input classes
     of DESIGN.md section 10; with non-finite inputs, differences confined to the rows / columns that hold them."""
     _ref()
-    sys.path.insert(0, os.path.join(ROOT, "tools", "probes"))
-    import fuzz_ref
-    out = fuzz_ref.sweep(300, mode["seed"], extreme=mode["extreme"], ab_mode=mode["ab_mode"], ld=mode["ld"],
+    out = sweep(300, mode["seed"], extreme=mode["extreme"], ab_mode=mode["ab_mode"], ld=mode["ld"],
                          verbose=False, ref_epi=mode.get("ref_epi", False))
     assert out["cases"] == 300
     assert not out["failures"], out["failures"][:3]
