@@ -20,6 +20,7 @@ row-block partition instead (rank r: the 8192-row block r of an (8192 N) x 8192 
 Prints ONE JSON line on rank 0.
 """
 import argparse
+import datetime
 import hashlib
 import json
 import os
@@ -61,12 +62,16 @@ def parse(argv=None):
     ap.add_argument("--moduli", type=int, default=None)
     ap.add_argument("--accurate", action="store_true")
     ap.add_argument("--partition", choices=["moduli", "rows"], default="moduli")
+    ap.add_argument("--order", choices=["moduli", "columns"], default="moduli",
+                    help="moduli partition: unit order of gemmul8.dist.ShardPlan")
     ap.add_argument("--gather", action="store_true", help="moduli partition: collect C on rank 0 in the step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--no-dgemm", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="sharded runs: skip timing the other partitions")
     ap.add_argument("--cpu-sample", type=int, default=0, help="CPU baseline size (default: auto)")
+    ap.add_argument("--no-single-gpu", action="store_true",
+                    help="sharded runs: skip timing the same call on one GPU after the timed region")
     return ap.parse_args(argv)
 
 
@@ -114,10 +119,13 @@ def dist_setup():
         sys.stdout.flush()
         saved = os.dup(1)
         os.dup2(2, 1)
+        # explicit communicator timeout: a peer that never arrives fails the run in minutes, not at the
+        # default watchdog's limit (GEMMUL8_DIST_TIMEOUT seconds, default 300)
+        tmo = datetime.timedelta(seconds=float(os.environ.get("GEMMUL8_DIST_TIMEOUT", "300")))
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=tmo)
         dist.barrier()  # the connections are up before stdout is given back
         world = dist.get_world_size()
         rank = dist.get_rank()
@@ -156,9 +164,11 @@ def _cpu_model():
     return "unknown CPU"
 
 
-def cpu_baseline(size_hint, dev):
+def cpu_baseline(size_hint, dev, gpu_C=None):
     """The oracle (CPU restatement, OpenMP) timed on a bounded sample of the cfg2 workload (same generator,
-    fast mode, N = 14) and cfg1 (SGEMM emulation 1024^3, N = 4, fast) in full, both on this host."""
+    fast mode, N = 14) and cfg1 (SGEMM emulation 1024^3, N = 4, fast) in full, both on this host.
+    gpu_C: the GPU line's C of the same call (column-major, (n, m) tensor): the oracle's C is compared with it
+    byte for byte, and its error is measured against the double-double reference GEMM (eval.hpp semantics)."""
     import numpy as np
     import gemmul8 as G
     sys.path.insert(0, ROOT)
@@ -171,14 +181,22 @@ def cpu_baseline(size_hint, dev):
     t0 = time.perf_counter()
     C = O.gemm(A, A, 14, True)
     dt = time.perf_counter() - t0
-    ref = A @ A
-    rel = np.abs(C - ref) / np.abs(ref)
+    affinity = len(os.sched_getaffinity(0))
     out = {"value": 2.0 * n ** 3 / dt / 1e12, "unit": "TFLOP/s", "cores": threads, "kind": "port",
            "sample": f"cfg2 workload at m=n=k={n} (DGEMM emulation, num_moduli=14, fast mode, reference "
                      f"generator seed 123456, A == B), one call ({dt:.1f} s) of the oracle/oz2_oracle.c "
                      f"restatement (int8 products on AVX-512 VNNI: {O.vnni()}) with {threads} OpenMP threads on "
-                     f"{_cpu_model()} ({os.cpu_count()} logical CPUs visible)",
-           "relerr_max_vs_fp64": float(rel.max()), "relerr_median_vs_fp64": float(np.median(rel))}
+                     f"{_cpu_model()} ({affinity} CPUs in this process's affinity mask, "
+                     f"{os.cpu_count()} logical CPUs in the machine)",
+           "threads": threads, "affinity_cpus": affinity, "logical_cpus_machine": os.cpu_count()}
+    dA = torch.from_numpy(np.ascontiguousarray(A.T)).to(dev)
+    C1, C2 = G.dd_gemm(dA, dA, n, n, n)
+    dC = torch.from_numpy(np.ascontiguousarray(C.T)).to(dev)
+    emax, emed = G.relerr_dd(dC, C1, C2)
+    out["relerr_max"], out["relerr_median"] = emax, emed  # against the double-double GEMM, as the GPU line
+    if gpu_C is not None and tuple(gpu_C.shape) == (n, n):
+        out["bit_identical_to_gpu_C"] = bool(torch.equal(gpu_C.view(torch.uint8), dC.view(torch.uint8)))
+    del C1, C2, dA, dC
     # cfg1 in full: SGEMM emulation 1024^3, N = 4, fast mode (BASELINE.json configs[0])
     A1 = G.randmat(1024, 1024, torch.float32, 0.5, 123456, dev).cpu().numpy().T
     t0 = time.perf_counter()
@@ -314,12 +332,59 @@ def labels(W):
     return workload, metric
 
 
+def algorithmic_work(m, n, k, N, kind, fast, L):
+    """SURVEY.md 8(d)'s algorithmic work of one call: int8 ops of the products this build runs (2 m n k per
+    plane; complex: 4 m n k big matrix, 3 m n k Karatsuba; accurate mode: one bound plane more) and the fused-
+    minimum HBM bytes per phase -- operands read once, slices written once and read once by the products,
+    residues written once and read once by the CRT, C written once (beta = 0).  Slice and residue bytes are
+    the padded planes of this build's layout (gemmul8.layout)."""
+    cplx = kind == "z"
+    eA, eB, eC = {"d": (8, 8, 8), "dfd": (8, 4, 8), "z": (16, 16, 16)}[kind]
+    fmac = (3.0 if L["nsub"] == 3 else 4.0) if cplx else 1.0
+    planes = N + (0 if fast else 1)
+    ops = 2.0 * fmac * m * n * k * planes
+    slices = N * (L["planeA"] + L["planeB"])
+    resid = N * L["planeR"]
+    split = m * k * eA + k * n * eB + slices + (0 if fast else L["planeA"] + L["planeB"])
+    prod = slices + resid + (0 if fast else L["planeA"] + L["planeB"])
+    crt = resid + m * n * eC
+    return {"int8_ops": ops, "bytes": {"split": split, "products": prod, "crt": crt,
+                                       "total": split + prod + crt}}
+
+
+def composite_roofline(work, ms_per_step, phase_ms=None, world=1):
+    """(int8_ops / P_int8 + bytes_alg / B_hbm) / t_step (world > 1: over W GPUs' peaks),
+    plus each memory-bound phase's algorithmic GB/s from its measured time"""
+    t = ms_per_step * 1e-3
+    t_mfma = work["int8_ops"] / (INT8_PEAK_TOPS * 1e12 * world)
+    t_hbm = work["bytes"]["total"] / (HBM_PEAK_GBS * 1e9 * world)
+    out = {"int8_ops": work["int8_ops"], "bytes_alg": work["bytes"]["total"],
+           "t_mfma_bound_ms": round(t_mfma * 1e3, 4), "t_hbm_bound_ms": round(t_hbm * 1e3, 4),
+           "frac": round((t_mfma + t_hbm) / t, 4),
+           "formula": "(int8_ops/P_int8 + bytes_alg/B_hbm)/t_step" + (f" with P, B x {world} GPUs" if world > 1 else "")}
+    if phase_ms:
+        gbs = {}
+        for name, key in (("split", "scaling"), ("crt", "inverse_scaling")):
+            if phase_ms.get(key, 0) > 0:
+                gbs[name] = {"bytes_alg": work["bytes"][name], "ms": phase_ms[key],
+                             "GBps": round(work["bytes"][name] / (phase_ms[key] * 1e-3) / 1e9, 1),
+                             "frac_of_hbm_peak": round(work["bytes"][name] / (phase_ms[key] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        out["phases"] = gbs
+    return out
+
+
 def main():
     args = parse()
     maybe_launch(args)
     world, rank, backend = dist_setup()
     import gemmul8 as G
     from gemmul8 import dist as GD
+
+    wd = None
+    if world > 1:
+        # fail fast: a phase that outlives its limit ends this rank with the stage and peers it was at
+        wd = GD.StageWatchdog(float(os.environ.get("GEMMUL8_DIST_WATCHDOG_S", "240")), rank)
+    arm = (lambda ph: wd.arm(ph)) if wd else (lambda ph: None)
 
     W = select_workload(args, world)
     wl_name, wl, m, N, fast, kind, custom = W["name"], W["wl"], W["m"], W["N"], W["fast"], W["kind"], W["custom"]
@@ -329,17 +394,28 @@ def main():
     flop_per = (8.0 if cplx else 2.0) * m * n * k
     dev = torch.device("cuda", torch.cuda.current_device())
     sharded = world > 1 and args.partition == "moduli"
+    rows_accurate = world > 1 and not sharded and not fast
     seed = 123456 + (rank if (world > 1 and not sharded) else 0)
+    arm("setup")
     A, B, tc = make_operands(kind, m, n, k, seed, dev)
+    L = G.layout(m, n, k, N, ct)
     trace = None
     if sharded:
         ops = GD.HipShardOps()
-        plan = GD.ShardPlan(m, n, N, world)
+        plan = GD.ShardPlan(m, n, N, world, order=args.order)
         trace = []
 
         def step(tr=None):
             return GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, tc, ct, gather=args.gather, ops=ops,
-                                  trace=tr)
+                                  trace=tr, order=args.order)
+    elif rows_accurate:
+        # accurate row blocks: B's column shifts come from the bound product over ALL rows of A, so the ranks
+        # MAX-combine its column maxima (gemmul8.dist.matmul_rows); row-major operands: op T on both
+        Arm, Brm = A.t().contiguous(), B.t().contiguous()
+        row_ops = GD.HipOps()
+
+        def step(tr=None):
+            return GD.matmul_rows(Arm, Brm, N, False, tc, ops=row_ops)
     else:
         C = torch.empty((n, m), dtype=tc, device=dev)
         work = G.alloc_work(m, n, k, N, ct, dev)
@@ -348,11 +424,13 @@ def main():
             G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, work, ct)
             return C
 
+    arm("warmup")
     for _ in range(args.warmup):
         step()
     G.timing_enable(True)
     G.timing_read()  # reset
     barrier(world)
+    arm("timed steps")
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(trace)
@@ -368,7 +446,8 @@ def main():
     avg = [x / args.steps for x in phase_ms]
     extra = {}
     # int8 MACs per output element and modulus relative to m n k: 1 real, 4 complex big matrix, 3 Karatsuba
-    fmac = (3.0 if G.layout(m, n, k, N, ct)["nsub"] == 3 else 4.0) if cplx else 1.0
+    fmac = (3.0 if L["nsub"] == 3 else 4.0) if cplx else 1.0
+    work_alg = algorithmic_work(m, n, k, N, kind, fast, L)
     if sharded:
         # dominant kernel: the int8 products of rank 0's units (one products_cols launch per merged unit)
         ops_step = sum(2.0 * m * (c1 - c0) * k * fmac * (j1 - j0) for j0, j1, c0, c1 in plan.launches[rank])
@@ -391,13 +470,21 @@ def main():
                 "kernel": G.last_products_kernel() + " (residue products; int8 ops counted as FLOP, "
                           "2*m'*n'*k' per plane and launch" + (", rank 0's units)" if sharded else ")"),
                 "avg_launch_ms": round(gemm_ms, 4)}
+    if sharded:
+        # every unit of the plan runs exactly once: all ranks' int8 ops over W GPUs' peak and the step time
+        # (accurate mode: the bound product is split by column blocks too)
+        roofline["aggregate"] = {"int8_ops_all_ranks": work_alg["int8_ops"],
+                                 "frac": round(work_alg["int8_ops"] / (world * INT8_PEAK_TOPS * 1e12 * ms_per_step * 1e-3), 4),
+                                 "formula": "sum over ranks of int8 ops / (W * P_int8 * t_step)"}
 
     if sharded and kind == "d" and not args.no_variants:
+        arm("variants")
         extra["variants"] = time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops)
 
     # accuracy against a double-double reference (testing/eval.hpp semantics); sharded: each rank checks
     # its own output columns, the max is combined
     if not args.no_accuracy and not cplx and kind == "d":
+        arm("accuracy")
         Cout = step()
         torch.cuda.synchronize()
         if sharded:
@@ -419,16 +506,45 @@ def main():
             extra["relerr_max"] = emax
             extra["relerr_median"] = emed
             del C1, C2
-            # a second, independent seed pair (A 123456, B 654321) beside the reference's A == B
-            B2 = G.randmat(k, n, torch.float64, 0.5, 654321, dev)
-            C2o = torch.empty((n, m), dtype=tc, device=dev)
-            G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B2, k, 0.0, C2o, m, N, fast, work, ct)
-            C1, C2 = G.dd_gemm(A, B2, m, n, k)
-            emax2, emed2 = G.relerr_dd(C2o, C1, C2)
-            extra["relerr_seed_pair_123456_654321"] = {"max": emax2, "median": emed2}
-            del C1, C2, B2, C2o
+            if world == 1:
+                # a second, independent seed pair (A 123456, B 654321) beside the reference's A == B
+                B2 = G.randmat(k, n, torch.float64, 0.5, 654321, dev)
+                C2o = torch.empty((n, m), dtype=tc, device=dev)
+                G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B2, k, 0.0, C2o, m, N, fast, work, ct)
+                C1, C2 = G.dd_gemm(A, B2, m, n, k)
+                emax2, emed2 = G.relerr_dd(C2o, C1, C2)
+                extra["relerr_seed_pair_123456_654321"] = {"max": emax2, "median": emed2}
+                del C1, C2, B2, C2o
+
+    if sharded and not args.no_single_gpu:
+        # the same call on ONE GPU (rank 0, after the timed region; the other ranks wait at the barrier): the
+        # strong-scaling efficiency of this line is single_gpu_ms / (W * ms_per_step)
+        arm("single-GPU baseline")
+        GD.release_workspaces(ops)
+        torch.cuda.empty_cache()
+        if rank == 0:
+            C1g = torch.empty((n, m), dtype=tc, device=dev)
+            w1 = G.alloc_work(m, n, k, N, ct, dev)
+            one = lambda: G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C1g, m, N, fast, w1, ct)
+            one()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 3
+            e0.record()
+            for _ in range(reps):
+                one()
+            e1.record()
+            torch.cuda.synchronize()
+            single_ms = e0.elapsed_time(e1) / reps
+            extra["single_gpu_ms"] = round(single_ms, 4)
+            extra["single_gpu_tflops"] = round(flop_per / (single_ms * 1e-3) / 1e12, 2)
+            extra["strong_scaling_efficiency"] = round(single_ms / (world * ms_per_step), 4)
+            del w1, C1g
+            torch.cuda.empty_cache()
+        barrier(world)
 
     if rank == 0:
+        arm("report")
         # measured live after the timed region: the same MFMA alone on uniformly random operand bytes
         # (the residue distribution) in registers -- the clock the chip holds under that load bounds
         # any int8 GEMM on such data
@@ -436,9 +552,12 @@ def main():
         if ceiling > 0:
             roofline["data_bound_ceiling"] = round(ceiling, 1)
             roofline["frac_of_data_bound_ceiling"] = round(achieved / ceiling, 4)
-        if not sharded:
+        if not sharded and not rows_accurate:
             extra["phase_ms"] = {"scaling": round(avg[0], 4), "int8_products": round(avg[1], 4),
                                  "inverse_scaling": round(avg[3], 4)}
+            roofline["composite"] = composite_roofline(work_alg, ms_per_step, extra["phase_ms"])
+        elif sharded:
+            roofline["composite"] = composite_roofline(work_alg, ms_per_step, None, world)
         if not args.no_dgemm and kind == "d" and (world == 1 or sharded):
             # the vendor DGEMM of the same shape on ONE GPU (rocBLAS through torch)
             Ar, Br = A.t(), B.t()
@@ -453,7 +572,8 @@ def main():
             dg = 2.0 * m * n * k * reps / (time.perf_counter() - t1) / 1e12
             extra["rocblas_dgemm_tflops_1gpu"] = round(dg, 2)
             extra["vs_rocblas_dgemm_1gpu"] = round(value / dg, 3)
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev)
+        gpu_C = C if (world == 1 and kind == "d" and fast and N == 14) else None
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev, gpu_C)
         workload, metric = labels(W)
         out = {
             "metric": metric,
@@ -464,7 +584,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "strong" if sharded else "weak",
+            "scaling": "strong" if sharded else ("weak" if world > 1 else "single"),
             "vs_baseline": round(value / world / GH200_PUBLISHED_TFLOPS, 3) if (wl_name == "cfg2" and not custom) else None,
             "vs_baseline_ref": "GH200 published OS2-fast-14 8192 (72.13 TFLOP/s, BASELINE.md); per-GPU ratio",
             "dtype": "i8",
@@ -480,12 +600,20 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if sharded:
+            out["config"]["unit_order"] = args.order
+            out["config"]["dist_side_stream"] = GD.side_stream_enabled() and backend == "nccl"
+            out["config"]["dist_timeout_s"] = float(os.environ.get("GEMMUL8_DIST_TIMEOUT", "300"))
         out.update(extra)
         print(json.dumps(out), flush=True)
     if world > 1:
         import torch.distributed as dist
+        arm("teardown")
         dist.barrier()
         dist.destroy_process_group()
+    if wd:
+        wd.disarm()
+        wd.close()
 
 
 if __name__ == "__main__":

@@ -127,15 +127,16 @@ struct LaneGuard {
         c.stB = c.st;
     }
 };
+// a failed fork / join would leave the operand lanes unordered: it fails the call (GEMMUL8_E_HIP)
 static void fork(const Call &c) {
     if (!c.lane) return;
-    (void)hipEventRecord(c.lane->fork, c.st);
-    (void)hipStreamWaitEvent(c.stB, c.lane->fork, 0);
+    hip_ok(hipEventRecord(c.lane->fork, c.st));
+    hip_ok(hipStreamWaitEvent(c.stB, c.lane->fork, 0));
 }
 static void join(const Call &c) {
     if (!c.lane) return;
-    (void)hipEventRecord(c.lane->join, c.stB);
-    (void)hipStreamWaitEvent(c.st, c.lane->join, 0);
+    hip_ok(hipEventRecord(c.lane->join, c.stB));
+    hip_ok(hipStreamWaitEvent(c.st, c.lane->join, 0));
 }
 
 // ---------------- phase timing (HIP events on the call's stream) ----------------
@@ -200,8 +201,8 @@ struct Phase {
     void end() {
         if (!on) return;
         PhaseEvents &e = g_phase_ev;
-        if (e.start) (void)hipEventRecord(e.start, e.st);
-        if (e.stop && !e.stop_taken) (void)hipEventRecord(e.stop, e.st);
+        if (e.start) hip_ok(hipEventRecord(e.start, e.st));
+        if (e.stop && !e.stop_taken) hip_ok(hipEventRecord(e.stop, e.st));
         g_phase_ev = PhaseEvents{};
         on = false;
     }

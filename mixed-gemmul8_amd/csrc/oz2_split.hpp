@@ -28,6 +28,14 @@ inline thread_local PhaseEvents g_phase_ev{};
 // code, so an error the application left pending on the thread is neither reported nor consumed)
 inline thread_local bool g_launch_failed = false;
 
+// a stream-ordering call of the library (fork / join event, phase marker): a failure is this call's
+inline void hip_ok(hipError_t rc) {
+    if (rc != hipSuccess) {
+        g_launch_failed = true;
+        (void)hipGetLastError();
+    }
+}
+
 template <typename... KArgs, typename... Args>
 inline void launch(void (*kernel)(KArgs...), dim3 grid, dim3 block, hipStream_t st, Args... args) {
     std::tuple<KArgs...> kargs(static_cast<KArgs>(args)...);

@@ -40,12 +40,27 @@ results bit-identical to the single-GPU ``gemmul8.gemm`` on the same inputs.
     the ranks combine those column maxima (n int32) with one MAX all-reduce before encoding.
 
 The compute steps go through an ``ops`` object (default: the native library); tests substitute
-a CPU implementation to exercise the communication pattern under gloo.  Workspaces are cached per
-shape on the ops object (one object serves one call at a time), so repeated calls allocate only
-their output.
+a CPU implementation to exercise the communication pattern under gloo.
+
+Workspaces.  The native ops keep the workspaces of the last ``WORKSPACE_CACHE`` shapes (default 2,
+least recently used evicted) so that a repeated call allocates only its output; at cfg3 one workspace
+is 11.5 GiB.  The default ops objects are per host thread, so two threads never share a workspace;
+one ops object serves one call at a time.  ``release_workspaces()`` frees every cached workspace of
+the calling thread's default ops (and of any ops objects passed to it).
+
+Fail-fast controls (environment):
+    GEMMUL8_DIST_SIDE_STREAM=0   post every transfer stage from the compute stream (default 1: the
+                                 receive-only stages from a side stream; ``side_stream_enabled()``)
+and ``StageWatchdog``, which ends the process with a message naming the stage and the peers in flight
+when a host phase outlives its limit (bench.py arms it around every multi-rank phase).
 """
+import collections
 import functools
 import math
+import os
+import sys
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -55,9 +70,83 @@ from . import (OP_N, OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, 
 
 __all__ = ["OP_N", "OP_T", "REAL_DEFAULT", "COMPLEX_BIG_MATRIX_ENCODE", "ShardPlan", "HipShardOps", "HipOps", "blocks",
            "moduli_partition", "row_partition", "gemm_moduli", "gemm_moduli_planes_to_root", "matmul_moduli",
-           "matmul_rows"]
+           "matmul_rows", "release_workspaces", "side_stream_enabled", "StageWatchdog", "progress"]
 
 TILE = 256  # product tile edge: column blocks of the product units start at multiples of it
+WORKSPACE_CACHE = 2  # workspaces (shapes) kept per native ops object
+
+
+def side_stream_enabled():
+    """GEMMUL8_DIST_SIDE_STREAM (default 1): receive-only transfer stages posted from a side stream"""
+    return os.environ.get("GEMMUL8_DIST_SIDE_STREAM", "1") != "0"
+
+
+# ------------------------------------------------------------------------------------------------
+# progress record + watchdog (fail fast instead of waiting for the communicator's own timeout)
+# ------------------------------------------------------------------------------------------------
+_PROGRESS = {"call": 0, "stage": "idle", "detail": "", "t": time.monotonic()}
+_PROGRESS_LOCK = threading.Lock()
+
+
+def progress(stage, detail=""):
+    """record the host step this rank is at (what the watchdog reports if the rank stalls)"""
+    with _PROGRESS_LOCK:
+        _PROGRESS.update(stage=stage, detail=detail, t=time.monotonic())
+
+
+class StageWatchdog:
+    """Ends the process (exit status 3) when an armed phase outlives `limit_s` seconds.
+
+    ``arm(phase)`` starts a phase; ``disarm()`` ends it.  The message on stderr names the phase, this rank's
+    last recorded step (``progress``: the transfer stage posted last and its peers) and how long ago it was
+    recorded.  The process exits with os._exit from the watchdog thread: no exec, nothing restarted."""
+
+    def __init__(self, limit_s, rank=0, out=None, exit=True):
+        self.limit_s, self.rank, self.out = float(limit_s), rank, out or sys.stderr
+        self._phase, self._since = None, 0.0
+        self._cv = threading.Condition()
+        self._stop = False
+        self.fired = None  # the message (tests pass exit=False)
+        self.exit = exit
+        self._thr = threading.Thread(target=self._run, name="gemmul8-watchdog", daemon=True)
+        self._thr.start()
+
+    def arm(self, phase):
+        with self._cv:
+            self._phase, self._since = phase, time.monotonic()
+            self._cv.notify()
+
+    def disarm(self):
+        with self._cv:
+            self._phase = None
+            self._cv.notify()
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._thr.join()
+
+    def _run(self):
+        with self._cv:
+            while not self._stop:
+                if self._phase is None:
+                    self._cv.wait()
+                    continue
+                left = self._since + self.limit_s - time.monotonic()
+                if left > 0:
+                    self._cv.wait(timeout=left)
+                    continue
+                with _PROGRESS_LOCK:
+                    p = dict(_PROGRESS)
+                msg = (f"gemmul8 watchdog: rank {self.rank} stuck in phase '{self._phase}' for more than "
+                       f"{self.limit_s:.0f} s; last step: call {p['call']} {p['stage']} {p['detail']} "
+                       f"({time.monotonic() - p['t']:.1f} s ago)")
+                self.fired = msg
+                print(msg, file=self.out, flush=True)
+                if self.exit:
+                    os._exit(3)
+                self._phase = None
 
 
 def blocks(n, parts, align=TILE):
@@ -93,6 +182,12 @@ def row_partition(m, world, align=256):
 class ShardPlan:
     """Who computes what in gemm_moduli (every rank builds the same plan).
 
+    order        how the N * cb units are dealt out in runs of N / g: "moduli" (modulus-major: a rank's units
+                 span about N / W moduli and every column block, so its residue columns go to all W - 1 peers,
+                 one W-th each) or "columns" (column-block-major: a rank's units are N / g moduli of ONE column
+                 block, so it reads and encodes only that block of op(B), but the moduli it encodes for the
+                 whole of op(A) grow to N / g, and its remote columns all go to the g - 1 other owners of the
+                 block -- one peer at W = 8, N = 14)
     units[r]     rank r's (modulus, c0, c1) product units
     cols[r]      rank r's output columns (its CRT, and the columns of op(B) whose shifts it computes)
     rows[r]      the rows of op(A) whose shifts rank r computes
@@ -104,12 +199,17 @@ class ShardPlan:
     mods[r]      the moduli range [j0, j1) whose slices rank r encodes
     """
 
-    def __init__(self, m, n, num_moduli, world, align=TILE):
-        self.m, self.n, self.N, self.world = m, n, num_moduli, world
+    def __init__(self, m, n, num_moduli, world, align=TILE, order="moduli"):
+        if order not in ("moduli", "columns"):
+            raise ValueError(f"unit order {order!r}: 'moduli' or 'columns'")
+        self.m, self.n, self.N, self.world, self.order = m, n, num_moduli, world, order
         g = math.gcd(num_moduli, world)
         self.col_blocks = world // g  # column blocks per modulus
         pcols = blocks(n, self.col_blocks, align)
-        units = [(j, c0, c1) for j in range(num_moduli) for (c0, c1) in pcols]
+        if order == "moduli":
+            units = [(j, c0, c1) for j in range(num_moduli) for (c0, c1) in pcols]
+        else:  # runs of N / g units never straddle a column block (N / g divides N), so moduli stay contiguous
+            units = [(j, c0, c1) for (c0, c1) in pcols for j in range(num_moduli)]
         per = len(units) // world  # = N / g
         self.units = [[u for u in units[r * per:(r + 1) * per] if u[2] > u[1]] for r in range(world)]
         self.cols = blocks(n, world, align)
@@ -155,24 +255,36 @@ class ShardPlan:
 
 
 @functools.lru_cache(maxsize=64)
-def _plan(m, n, num_moduli, world, align):
-    return ShardPlan(m, n, num_moduli, world, align)
+def _plan(m, n, num_moduli, world, align, order="moduli"):
+    return ShardPlan(m, n, num_moduli, world, align, order)
 
 
 # ------------------------------------------------------------------------------------------------
 # native compute steps
 # ------------------------------------------------------------------------------------------------
 class _WorkCache:
-    """workspaces per key, reused across calls (no workspace allocation in a timed loop)"""
+    """workspaces per key, reused across calls (no workspace allocation in a timed loop); at most `cap`
+    workspace entries are kept, the least recently used one is dropped first (other entries: unbounded)"""
 
-    def __init__(self):
-        self._d = {}
+    def __init__(self, cap=None):
+        self._d = collections.OrderedDict()
+        self.cap = cap
 
     def get(self, key, make):
         t = self._d.get(key)
         if t is None:
+            if key[0] == "work":
+                cap = WORKSPACE_CACHE if self.cap is None else self.cap
+                works = [kk for kk in self._d if kk[0] == "work"]
+                for kk in works[:max(0, len(works) - cap + 1)]:
+                    del self._d[kk]  # (released before the new one is allocated)
             t = self._d[key] = make()
+        else:
+            self._d.move_to_end(key)
         return t
+
+    def keys(self):
+        return list(self._d)
 
     def clear(self):
         self._d.clear()
@@ -245,14 +357,30 @@ class HipShardOps:
         torch.cuda.current_stream().synchronize()
 
 
-_default_shard_ops = None
+_DEFAULT = threading.local()  # the default ops objects, one set per host thread
 
 
 def _shard_ops():
-    global _default_shard_ops
-    if _default_shard_ops is None:
-        _default_shard_ops = HipShardOps()
-    return _default_shard_ops
+    ops = getattr(_DEFAULT, "shard", None)
+    if ops is None:
+        ops = _DEFAULT.shard = HipShardOps()
+    return ops
+
+
+def _row_ops():
+    ops = getattr(_DEFAULT, "rows", None)
+    if ops is None:
+        ops = _DEFAULT.rows = HipOps()
+    return ops
+
+
+def release_workspaces(*ops_objects):
+    """Free the cached workspaces (and side streams) of the calling thread's default ops and of `ops_objects`;
+    the next call allocates afresh.  The memory returns to torch's caching allocator
+    (torch.cuda.empty_cache() hands it back to the device)."""
+    for o in (getattr(_DEFAULT, "shard", None), getattr(_DEFAULT, "rows", None)) + ops_objects:
+        if o is not None:
+            o.cache.clear()
 
 
 def _group_info(group):
@@ -296,20 +424,24 @@ def _allgather_blocks(vecs, blks, rank, group):
 
 
 def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
-                computeType=REAL_DEFAULT, group=None, gather=False, root=0, ops=None, align=TILE, trace=None):
+                computeType=REAL_DEFAULT, group=None, gather=False, root=0, ops=None, align=TILE, trace=None,
+                order="moduli"):
     """C = op(A) op(B) (column-major operands, alpha = 1, beta = 0) with the work split over the ranks of
     `group` by (modulus, column block) units; A and B replicated on every rank.
 
     Returns this rank's output columns [c0, c1) = ShardPlan.cols[rank] as an (c1 - c0, m) tensor (the
     column-major m x (c1 - c0) block), or with gather=True the whole (n, m) C on the root and None elsewhere.
     trace: a list that receives (phase, torch.cuda.Event) pairs recorded on the current stream at the phase
-    boundaries (start, shifts, encode, products, exchange, crt)."""
+    boundaries (start, shifts, encode, products, exchange, crt).  order: ShardPlan's unit order."""
     ops = ops or _shard_ops()
     out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
     rank, world = _group_info(group)
-    plan = _plan(m, n, num_moduli, world, align)  # (align: the native products need TILE)
+    plan = _plan(m, n, num_moduli, world, align, order)  # (align: the native products need TILE)
     # the gloo backend reads device tensors without waiting on the compute stream
     host_sync = dist.get_backend(group) != "nccl"
+    with _PROGRESS_LOCK:
+        _PROGRESS["call"] += 1
+    progress("shifts", f"all-gather of {m} + {n} int16 over {world} ranks")
     st = ops.prepare(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, out_dtype, computeType)
     c0, c1 = plan.cols[rank]
 
@@ -337,6 +469,7 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
     # 2. slices of this rank's moduli (accurate mode derives the final shifts here too, from sft0 and the bound
     # maxima: a rank without moduli still needs them for the CRT of its columns)
     j0, j1 = plan.mods[rank]
+    progress("encode", f"moduli [{j0}, {j1})")
     if j1 > j0 or not fastmode:
         ops.encode(st, j0, j1)
     mark("encode")
@@ -347,19 +480,24 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
     # that it does not wait for this rank's remaining products
     reqs = []
     mine = plan.launches[rank]
-    side = None if host_sync else ops.side_stream()
+    side = None if (host_sync or not side_stream_enabled()) else ops.side_stream()
     if side is not None:
         # ... but after everything enqueued before this call (the previous call's CRT reads these columns)
         side.wait_stream(torch.cuda.current_stream())
     for t in range(plan.stages):
         if t < len(mine):
+            progress(f"products stage {t}", "launch (j0, j1, c0, c1) = %s" % (mine[t],))
             ops.products(st, *mine[t])
+        sends, recvs = plan.sends(rank, t), plan.recvs(rank, t)
         snd = [dist.P2POp(dist.isend, x, _global(group, dst), group)
-               for dst, j, a, b in plan.sends(rank, t) for x in ops.chunks(st, j, a, b)]
+               for dst, j, a, b in sends for x in ops.chunks(st, j, a, b)]
         rcv = [dist.P2POp(dist.irecv, x, _global(group, src), group)
-               for src, j, a, b in plan.recvs(rank, t) for x in ops.chunks(st, j, a, b)]
+               for src, j, a, b in recvs for x in ops.chunks(st, j, a, b)]
         if not snd and not rcv:
             continue
+        progress(f"exchange stage {t}", "sends to %s, receives from %s (%s stream)" % (
+            sorted({x[0] for x in sends}), sorted({x[0] for x in recvs}),
+            "side" if (side is not None and not snd) else "compute"))
         if host_sync:
             ops.sync()
         if snd or side is None:
@@ -368,13 +506,16 @@ def gemm_moduli(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True,
             with torch.cuda.stream(side):
                 reqs += dist.batch_isend_irecv(rcv)
     mark("products")
+    progress("exchange wait", f"{len(reqs)} grouped transfer calls")
     for q in reqs:
         q.wait()
     mark("exchange")
 
     # 5. CRT of this rank's output columns
+    progress("crt", f"columns [{c0}, {c1})")
     Cb = ops.recombine(st, c0, c1)
     mark("crt")
+    progress("done")
     if not gather:
         return Cb
     if host_sync:
@@ -442,17 +583,19 @@ def gemm_moduli_planes_to_root(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14,
 
 
 def matmul_moduli(A, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, gather=True, root=0, ops=None,
-                  align=TILE):
+                  align=TILE, order="moduli"):
     """C = A @ B (row-major torch tensors, A, B replicated) sharded over the ranks of `group` (gemm_moduli).
 
     gather=True: the whole C (m x n) on the root, None elsewhere; gather=False: this rank's column block
-    C[:, c0:c1] as an (c1 - c0) x m tensor holding its transpose (the column-major block)."""
+    C[:, c0:c1] (c0, c1 = ShardPlan.cols[rank]) as an m x (c1 - c0) tensor, a transposed view of the
+    column-major buffer.  The default ops cache this shape's workspace (see the module docstring;
+    release_workspaces() frees it)."""
     m, k = A.shape
     n = B.shape[1]
     ct = COMPLEX_BIG_MATRIX_ENCODE if A.is_complex() else REAL_DEFAULT
     # a row-major (m x k) tensor is the column-major k x m matrix: op T on both operands, no copies
     out = gemm_moduli(OP_T, OP_T, m, n, k, A.contiguous(), k, B.contiguous(), n, num_moduli, fastmode, out_dtype, ct,
-                      group, gather, root, ops, align)
+                      group, gather, root, ops, align, order=order)
     return None if out is None else out.t()
 
 
@@ -504,20 +647,14 @@ class HipOps:
         torch.cuda.current_stream().synchronize()
 
 
-_default_row_ops = None
-
-
 def matmul_rows(A_local, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, gather=False, root=0,
                 ops=None):
     """C_local = A_local @ B on this rank (A_local: this rank's rows, B replicated).
 
     With gather=True the root returns the full C (rows concatenated in rank order) and the
-    other ranks return None."""
-    global _default_row_ops
-    if ops is None:
-        if _default_row_ops is None:
-            _default_row_ops = HipOps()
-        ops = _default_row_ops
+    other ranks return None.  The default ops cache this shape's workspace (see the module docstring;
+    release_workspaces() frees it)."""
+    ops = ops or _row_ops()
     out_dtype = out_dtype or torch.promote_types(A_local.dtype, B.dtype)
     rank, world = _group_info(group)
     if fastmode or world == 1:

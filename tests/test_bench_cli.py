@@ -49,3 +49,40 @@ def test_workload_selection_and_labels():
     assert "accurate" in b.labels(W)[1]
     W = b.select_workload(b.parse(["--workload", "cfg5"]), 1)
     assert (W["m"], W["N"], W["kind"]) == (4096, 12, "z") and "ZGEMM" in b.labels(W)[1]
+
+
+def test_algorithmic_work_and_composite_roofline():
+    """cfg2's fused-minimum bytes (operands once, slices and residues written and read once,
+    C once) and the composite fraction; the per-phase GB/s follow from phase_ms"""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd"))
+    import gemmul8 as G
+    b = _bench()
+    L = G.layout(8192, 8192, 8192, 14, G.REAL_DEFAULT)
+    w = b.algorithmic_work(8192, 8192, 8192, 14, "d", True, L)
+    mk = 8192 * 8192
+    assert w["int8_ops"] == 2.0 * mk * 8192 * 14
+    assert w["bytes"]["split"] == 2 * 8 * mk + 14 * 2 * mk
+    assert w["bytes"]["products"] == 14 * 2 * mk + 14 * mk
+    assert w["bytes"]["crt"] == 14 * mk + 8 * mk
+    assert abs(w["bytes"]["total"] - 7.248e9) < 0.01e9  # SURVEY 8(d): 7.28 GB with the reference's k' = 8256
+    c = b.composite_roofline(w, 6.0, {"scaling": 0.7, "inverse_scaling": 0.27})
+    t_m, t_h = w["int8_ops"] / (b.INT8_PEAK_TOPS * 1e12), w["bytes"]["total"] / (b.HBM_PEAK_GBS * 1e9)
+    assert abs(c["frac"] - (t_m + t_h) / 6e-3) < 1e-4
+    assert abs(c["phases"]["split"]["GBps"] - w["bytes"]["split"] / 0.7e-3 / 1e9) < 0.1
+    assert abs(c["phases"]["crt"]["GBps"] - w["bytes"]["crt"] / 0.27e-3 / 1e9) < 0.1
+    # over W GPUs the same work is priced against W peaks
+    c8 = b.composite_roofline(w, 6.0 / 8, None, 8)
+    assert abs(c8["frac"] - c["frac"]) < 1e-3 and "phases" not in c8
+    # accurate mode: the bound plane and its magnitude slices on top
+    La = G.layout(8192, 8192, 8192, 10, G.REAL_DEFAULT)
+    wa = b.algorithmic_work(8192, 8192, 8192, 10, "dfd", False, La)
+    assert wa["int8_ops"] == 2.0 * mk * 8192 * 11
+    assert wa["bytes"]["split"] == 8 * mk + 4 * mk + 10 * 2 * mk + 2 * mk
+
+
+def test_new_bench_options():
+    b = _bench()
+    a = b.parse(["--gpus", "2", "--order", "columns", "--no-single-gpu"])
+    assert a.order == "columns" and a.no_single_gpu
+    assert b.parse([]).order == "moduli" and not b.parse([]).no_single_gpu

@@ -117,16 +117,18 @@ def _worker(rank, world, port, case, outdir):
     from gemmul8 import dist as GD
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        m, n, k, N, fast, dt = case
+        m, n, k, N, fast, dt = case[:6]
+        order = case[6] if len(case) > 6 else "moduli"
         rng = np.random.default_rng(7)
         A = ((rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))).astype(dt)
         B = ((rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))).astype(dt)
         ops = OracleOps()
         # small column blocks (align 16) so that every rank owns units and output columns
-        Cm = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, ops=OracleShardOps(), align=16)
+        Cm = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, ops=OracleShardOps(), align=16,
+                              order=order)
         # the column block of this rank without the gather (C stays distributed)
         Cb = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, gather=False, ops=OracleShardOps(),
-                              align=16)
+                              align=16, order=order)
         np.save(os.path.join(outdir, f"block{rank}.npy"), Cb.contiguous().numpy())
         # SURVEY 8(e) variant (i): whole moduli per rank, planes gathered on the root
         Cp = GD.gemm_moduli_planes_to_root(1, 1, m, n, k, torch.from_numpy(A), k, torch.from_numpy(B), n, N, fast,
@@ -159,12 +161,15 @@ def _worker(rank, world, port, case, outdir):
     (8, (60, 130, 40, 9, False, np.float64)),
     (7, (90, 45, 50, 3, False, np.float64)),   # accurate: rank 1 multiplies no modulus but owns columns
     (3, (40, 50, 61, 7, False, np.complex128)),
+    (8, (120, 300, 64, 14, True, np.float64, "columns")),  # column-block-major units: 7 moduli x 1 block each
+    (4, (100, 70, 64, 14, False, np.float64, "columns")),
+    (3, (48, 30, 50, 9, True, np.complex128, "columns")),
 ])
 def test_sharded_equals_single_call(tmp_path, world, case):
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     mp.spawn(_worker, args=(world, _free_port(), case, str(tmp_path)), nprocs=world, join=True)
-    m, n, k, N, fast, dt = case
+    m, n, k, N, fast, dt = case[:6]
     rng = np.random.default_rng(7)
     A = ((rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))).astype(dt)
     B = ((rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))).astype(dt)
@@ -174,7 +179,7 @@ def test_sharded_equals_single_call(tmp_path, world, case):
         assert got.shape == C.shape
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C).view(np.uint8)), name
     from gemmul8.dist import ShardPlan
-    for r, (c0, c1) in enumerate(ShardPlan(m, n, N, world, 16).cols):
+    for r, (c0, c1) in enumerate(ShardPlan(m, n, N, world, 16, case[6] if len(case) > 6 else "moduli").cols):
         got = np.load(tmp_path / f"block{r}.npy")
         assert got.shape == (m, c1 - c0)
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C[:, c0:c1]).view(np.uint8)), r

@@ -151,6 +151,24 @@ def test_dist_one_rank_rccl():
         refa = _single(A, B, N, False, torch.float64)
         assert _same(GD.matmul_rows(A, B, N, False), refa)
         assert _same(GD.matmul_moduli(A, B, N, False), refa)
+        # the same shape again with other operands through the cached default workspace: accurate mode
+        # depends on the bound area being zeroed by every call
+        A2, B2 = _rand(m, k, 15, torch.float64) * 1e3, _rand(k, n, 16, torch.float64)
+        assert _same(GD.matmul_moduli(A2, B2, N, False), _single(A2, B2, N, False, torch.float64))
+        assert _same(GD.matmul_moduli(A, B, N, False), refa)
+        assert _same(GD.matmul_moduli(A, B, N, False, order="columns"), refa)
+        os.environ["GEMMUL8_DIST_SIDE_STREAM"] = "0"
+        try:
+            assert _same(GD.matmul_moduli(A2, B2, N, True), _single(A2, B2, N, True, torch.float64))
+        finally:
+            del os.environ["GEMMUL8_DIST_SIDE_STREAM"]
+        # the default ops keep at most WORKSPACE_CACHE workspaces, and release_workspaces frees them
+        for mm in (264, 296, 328):
+            GD.matmul_moduli(_rand(mm, k, 7, torch.float64), B, N, True)
+        works = [kk for kk in GD._shard_ops().cache.keys() if kk[0] == "work"]
+        assert len(works) == GD.WORKSPACE_CACHE and works[-1][1] == 328
+        GD.release_workspaces()
+        assert GD._shard_ops().cache.keys() == [] and GD._row_ops().cache.keys() == []
     finally:
         dist.destroy_process_group()
 
