@@ -181,6 +181,23 @@ def test_mixed_accurate(N):
     check_full(B.T.copy().astype(np.float32), A.T.copy(), N, fast=False)
 
 
+@pytest.mark.parametrize("m,n,k,N,tb,opB", [
+    (700, 1400, 16000, 10, np.float32, 0),   # the cfg4 form (f64 x f32), ragged last column tile
+    (512, 2048, 16384, 12, np.float64, 0),
+    (600, 1300, 16000, 8, np.float64, 1),    # op(B) = T: strided columns
+    (300, 600, 40000, 14, np.float64, 0),
+])
+def test_accurate_two_streams(m, n, k, N, tb, opB):
+    """Accurate mode at (m + n) k >= 2^25, where operand B's passes run on the second stream (the lane):
+    shifts, every slice, residues and C against the oracle, long k, ragged column tiles."""
+    rng = np.random.default_rng(m + n + k)
+    A = randmat_np(rng, m, k)
+    B = randmat_np(rng, k, n, dtype=tb)
+    if opB:
+        B = np.asfortranarray(B.T)
+    check_full(A, B, N, fast=False, opB=opB)
+
+
 @pytest.mark.parametrize("N", [6, 12])
 def test_zgemm_bigmatrix(N):
     rng = np.random.default_rng(55 + N)
