@@ -262,6 +262,14 @@ static ModParams sub_mod_params(unsigned N, unsigned j0, unsigned j1) {
     return P;
 }
 
+static bool one_read_magnitudes() {
+    static const bool on = [] {
+        const char *e = getenv("GEMMUL8_ONE_READ_MAGNITUDES");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 // accurate mode, first half of phase 1: sft0 = 5 - ilogb(amax), the 6-bit magnitude planes and the
 // bound product's row / column maxima (scaling.hpp:3053-3100).  A on the call's stream, B on the lane.
 // Sharded form (gemmul8_shard_bound): sft0 already assembled in the workspace (sft0_ready) and the
@@ -273,13 +281,23 @@ static void phase_bound(const Call &c, const Views &v, size_t c0 = 0, size_t c1 
     const Layout L = v.L.kara ? make_layout(c.m, c.n, c.k, c.N, c.cplx, v.L.S, 0) : v.L;
     const ModParams MP = make_mod_params(c.N);
     fork(c);
-    if (!sft0_ready) split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
-    split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
-    if (!sft0_ready) split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.stB);
-    // big-matrix B magnitudes carry the reference's tail defect; classic / Karatsuba do not
-    // the B tail defect lives in the op-N big-matrix extraction only (scaling.hpp:2312-2323, 3201-3203)
-    split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.stB,
-                 c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE && c.B.contig);
+    // real operands: sft0 and the magnitudes from one read of each operand (split_magnitudes), with the
+    // per-tile exponents in slice plane 1, unused until the final encode (GEMMUL8_ONE_READ_MAGNITUDES=0: the
+    // reference's two reads, for A/B runs)
+    const size_t s1A = v.L.S >= 2 ? L.planeA : 0, s1B = v.L.S >= 2 ? L.planeB : 0;
+    if (sft0_ready || !one_read_magnitudes() ||
+        !split_magnitudes(c.A, true, c.m, c.k, v.sft0, v.A8, L, v.A8 + L.planeA, s1A, c.st)) {
+        if (!sft0_ready) split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
+        split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
+    }
+    if (sft0_ready || !one_read_magnitudes() ||
+        !split_magnitudes(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L, v.B8 + L.planeB, s1B, c.stB)) {
+        if (!sft0_ready) split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.stB);
+        // big-matrix B magnitudes carry the reference's tail defect; classic / Karatsuba do not
+        // the B tail defect lives in the op-N big-matrix extraction only (scaling.hpp:2312-2323, 3201-3203)
+        split_encode(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L.planeB, L, 1, MP, c.stB,
+                     c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE && c.B.contig);
+    }
     join(c);
     zero_i32(v.bound, L.m_pad + L.n_pad, c.st);
     if (c1 > c.n) c1 = c.n;

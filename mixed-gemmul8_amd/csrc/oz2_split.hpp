@@ -81,6 +81,11 @@ void split_stats(const OperandDesc &d, size_t len, size_t nvec, int VT, bool acc
 void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, const int16_t *sft, int8_t *out,
                   size_t plane, const Layout &L, int mode, const ModParams &MP, hipStream_t st,
                   bool btail_quirk = false);
+// accurate mode, real operands: sft0 (as split_stats(accurate)) and the 6-bit magnitude plane (as split_encode
+// MODE 1) from one read of the operand; scratch: (kblk / 64) * round_up(vpad, 64) int2 of per-tile exponents
+// (false: not applicable -- complex, or scratch too small -- nothing launched)
+bool split_magnitudes(const OperandDesc &d, bool is_A, size_t nvec, size_t len, int16_t *sft0, int8_t *out,
+                      const Layout &L, void *scratch, size_t scratch_bytes, hipStream_t st);
 // fast-mode shifts of A (real f64 rows, strided) and B (real f64 columns, contiguous) in one launch
 // (false: not applicable, nothing launched)
 bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,

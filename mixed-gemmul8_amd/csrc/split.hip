@@ -15,6 +15,8 @@
 //              16-byte chunks straight into the MFMA-ready panel layout.
 // Accurate mode adds the 6-bit magnitude extraction (scaling.hpp:1897-1941,
 // 2215-2260) whose bound product runs on the int8 GEMM kernel (gemm_i8.hip).
+#include <climits>
+
 #include "oz2_split.hpp"
 #include <cstdlib>
 
@@ -763,6 +765,188 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_kernel(const R *__res
                                              blockIdx.x, blockIdx.y, tile);
 }
 
+// ------------------------------------------------------------------
+// Accurate mode, real operands: sft0 and the 6-bit magnitudes in ONE read of the operand.
+// The reference (scaling.hpp:1897-1941, 2215-2260) scales every element of a vector by 2^sft0,
+// sft0 = 5 - ilogb(amax of the vector), so it needs the amax before the first magnitude and reads the
+// vector twice.  Pass 1 (mag_tile_kernel) stages the encode's 64-vector x 64-element tiles and scales each
+// vector's 64 elements of a tile by the TILE's amax instead: m_t = ceil(|x| 2^(5 - e_t)), e_t = ilogb(tile
+// amax) <= e_v = ilogb(vector amax), recording e_t and the least exponent e_min of the tile's nonzero
+// elements per (tile, vector).  For real x > 0 and an integer d >= 0, ceil(ceil(x) / 2^d) = ceil(x / 2^d), so
+// pass 2 (mag_fixup_kernel) turns m_t into the reference's byte with integer arithmetic,
+// (m_t + 2^d - 1) >> d with d = e_v - e_t (d >= 7: m_t > 0, as m_t <= 64), provided the reference's scaled
+// values are exact: no element of the tile is subnormal under the final scale (e_min + 5 - e_v >= the least
+// normal exponent).  Tiles where that fails (a dynamic range beyond ~2^1000 (f64) / 2^120 (f32) inside one
+// vector, an infinite vector amax) and tiles holding a NaN are recomputed by pass 2 from the operand with the
+// final shift, exactly as encode_vec16's MODE 1.  Pass 2 reads and writes the magnitude plane (1 byte per
+// element) instead of re-reading the operand (8 or 4 bytes per element) and writes sft0 -- the same sft0 and
+// bytes as split_stats(accurate) + split_encode(MODE 1) (tests/test_gpu_parity.py, accurate cases).
+// tinfo codes: e_t = INT_MIN for a tile whose amax is 0; e_min = INT_MAX without a nonzero finite element,
+// INT_MIN with a NaN.
+constexpr int TI_ZERO = INT_MIN, TI_NAN = INT_MIN, TI_NONE = INT_MAX;
+
+// sft0_of(vector amax) from e_v = ilogb(amax) = max over the tiles of ilogb(tile amax)
+template <typename R> __device__ __forceinline__ int16_t sft0_of_exp(int ev) {
+    return ev == TI_ZERO ? sft0_of<R>(R(0)) : ev == INT_MAX ? SFT0_INF : (int16_t)(5 - ev);
+}
+
+template <typename R> __device__ __forceinline__ int mag_byte(R y) {
+    return std::is_same<R, double>::value ? __double2int_ru((double)y) : __float2int_ru((float)y);
+}
+
+template <typename R, bool CONTIG, bool NTL>
+__global__ __launch_bounds__(256) void mag_tile_kernel(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                                        int8_t *__restrict__ out, size_t ksteps,
+                                                        int2 *__restrict__ tinfo, size_t tstride, int flags) {
+    __shared__ EncTile<R, false> tile;
+    const bool kfirst = CONTIG && (flags & ENC_KFIRST);
+    const size_t kt = kfirst ? blockIdx.x : blockIdx.y;
+    const size_t v0 = (size_t)(kfirst ? blockIdx.y : blockIdx.x) * 64, e0 = kt * 64;
+    const int tid = threadIdx.x;
+    constexpr int NL = 16;  // 64 x 64 / 256
+    const bool interior = v0 + 64 <= nvec && e0 + 64 <= len;
+    R lre[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const int idx = tid + 256 * i;
+        const int el = CONTIG ? idx % 64 : idx >> 6, vl = CONTIG ? idx / 64 : idx & 63;
+        const size_t v = v0 + vl, e = e0 + el;
+        R im;
+        lre[i] = 0;
+        if (interior || (v < nvec && e < len)) load_elem<R, false, NTL>(X, CONTIG ? v * ld + e : e * ld + v, lre[i], im);
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+        const int idx = tid + 256 * i;
+        const int el = CONTIG ? idx % 64 : idx >> 6, vl = CONTIG ? idx / 64 : idx & 63;
+        tile[el][vl][0] = lre[i];
+    }
+    __syncthreads();
+    // the 4 lanes of a vector's tile row are neighbours in one wave (c-th 16-element chunk): its tile
+    // amax / least nonzero / NaN flag by two lane exchanges, no second block barrier
+    const int vl = tid >> 2, c = tid & 3;
+    R x[16], mx = 0, mn = R(INFINITY);
+    int nan = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        x[q] = fabs(tile[16 * c + q][vl][0]);
+        mx = fmax(mx, x[q]);  // NaN ignored, as the stats pass's amax
+        if (x[q] != R(0) && x[q] < mn) mn = x[q];
+        nan |= __builtin_isnan(x[q]) ? 1 : 0;
+    }
+#pragma unroll
+    for (int sh = 1; sh <= 2; sh <<= 1) {
+        mx = fmax(mx, __shfl_xor(mx, sh));
+        mn = fmin(mn, __shfl_xor(mn, sh));
+        nan |= __shfl_xor(nan, sh);
+    }
+    const R amax = mx, amin = mn;
+    const bool anan = nan != 0;
+    // the tile's scale: sft0_scale of sft0_of(tile amax) (for an Inf amax 5 - ilogb(Inf), the reference's int)
+    const int s = amax == R(0) ? 0 : 5 - ilogb_r<R>(amax);
+    uint32_t w[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        uint32_t a = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) a |= ((uint32_t)mag_byte<R>(scalbn(x[4 * d + b], s)) & 0xffu) << (8 * b);
+        w[d] = a;
+    }
+    const size_t v = v0 + vl;
+    *reinterpret_cast<uint4 *>(out + panel_offset(v, e0 + 16 * c, ksteps)) = make_uint4(w[0], w[1], w[2], w[3]);
+    if (c == 0 && v < tstride) {
+        const int et = amax == R(0) ? TI_ZERO : __builtin_isinf(amax) ? INT_MAX : ilogb_r<R>(amax);
+        const int em = anan ? TI_NAN : amin == R(INFINITY) ? TI_NONE : ilogb_r<R>(amin);
+        tinfo[kt * tstride + v] = make_int2(et, em);
+    }
+}
+
+// the vector exponent e_v = max over its tiles of e_t (= ilogb of the vector amax) and sft0 = sft0_of(amax):
+// 64 vectors x 4 tile slices per block
+template <typename R>
+__global__ __launch_bounds__(256) void mag_vexp_kernel(size_t nvec, size_t ktiles, const int2 *__restrict__ tinfo,
+                                                        size_t tstride, int *__restrict__ vexp,
+                                                        int16_t *__restrict__ sft0_out) {
+    __shared__ int part[4][64];
+    const int vl = threadIdx.x & 63, sl = threadIdx.x >> 6;
+    const size_t v = (size_t)blockIdx.x * 64 + vl;
+    int ev = INT_MIN;
+    if (v < nvec) {
+        constexpr int U = 8;  // loads in flight per thread
+        size_t t = sl;
+        for (; t + 4 * (U - 1) < ktiles; t += 4 * U) {
+            int e[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) e[u] = tinfo[(t + 4 * u) * tstride + v].x;
+#pragma unroll
+            for (int u = 0; u < U; ++u) ev = max(ev, e[u]);
+        }
+        for (; t < ktiles; t += 4) ev = max(ev, tinfo[t * tstride + v].x);
+    }
+    part[sl][vl] = ev;
+    __syncthreads();
+    if (sl == 0 && v < nvec) {
+        ev = max(max(part[0][vl], part[1][vl]), max(part[2][vl], part[3][vl]));
+        vexp[v] = ev;
+        sft0_out[v] = sft0_of_exp<R>(ev);
+    }
+}
+
+// one wave per (32 vectors, k-tile): lane (r, h) handles vector v0 + r and the 16-byte chunk h of each
+// 32-element half of the tile, so a wave's chunk accesses are 1 KiB contiguous in the panel layout
+template <typename R, bool CONTIG>
+__global__ __launch_bounds__(256) void mag_fixup_kernel(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                                         int8_t *__restrict__ out, size_t ksteps, size_t ktiles,
+                                                         const int2 *__restrict__ tinfo, size_t tstride,
+                                                         const int *__restrict__ vexp) {
+    const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+    const size_t v = (size_t)blockIdx.x * 32 + r;
+    const size_t t = (size_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (v >= nvec || t >= ktiles) return;  // padding vectors: pass 1 wrote their zeros
+    uint4 *p0 = reinterpret_cast<uint4 *>(out + panel_offset(v, t * 64 + h * 16, ksteps));
+    uint4 *p1 = reinterpret_cast<uint4 *>(out + panel_offset(v, t * 64 + 32 + h * 16, ksteps));
+    // the bytes are loaded before they are known to be needed: one memory round trip instead of two (the
+    // test on b0.x & b1.x, never all ones as every byte is <= 64, keeps the compiler from sinking the loads
+    // below the branches)
+    const uint4 b0 = *p0, b1 = *p1;
+    const int ev = vexp[v];
+    const int2 ti = tinfo[t * tstride + v];
+    const bool final_bytes = (ti.x == ev && ti.y != TI_NAN)          // d = 0 (the vector's own amax tile)
+                             || (ti.x == TI_ZERO && ti.y == TI_NONE);  // zeros only
+    if (final_bytes && (b0.x & b1.x) != ~0u) return;
+    const int srow = sft0_scale<R>(sft0_of_exp<R>(ev));  // (as mag_vexp_kernel stored it: no third load)
+    constexpr long long EMIN = std::is_same<R, double>::value ? -1022 : -126;
+    const bool exact = ti.y != TI_NAN && ev != INT_MAX && (ti.y == TI_NONE || (long long)ti.y + srow >= EMIN);
+    if (exact) {
+        const int d = min(ev - ti.x, 7);  // (m_t <= 64: from d = 7 on every nonzero byte becomes 1)
+        const uint32_t add = ((1u << d) - 1u) * 0x01010101u, mask = (0xffu >> d) * 0x01010101u;
+        // bytes <= 64: the byte-wise add cannot carry
+        *p0 = make_uint4(((b0.x + add) >> d) & mask, ((b0.y + add) >> d) & mask, ((b0.z + add) >> d) & mask,
+                         ((b0.w + add) >> d) & mask);
+        *p1 = make_uint4(((b1.x + add) >> d) & mask, ((b1.y + add) >> d) & mask, ((b1.z + add) >> d) & mask,
+                         ((b1.w + add) >> d) & mask);
+        return;
+    }
+    // the reference's own arithmetic with the final shift (encode_vec16, MODE 1)
+    for (int half = 0; half < 2; ++half) {
+        const size_t kk = t * 64 + half * 32 + h * 16;
+        uint32_t w[4];
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+            uint32_t a = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const size_t e = kk + 4 * dd + b;
+                R re = 0, im;
+                if (e < len) load_elem<R, false, false>(X, CONTIG ? v * ld + e : e * ld + v, re, im);
+                a |= ((uint32_t)mag_byte<R>(scalbn(fabs(re), srow)) & 0xffu) << (8 * b);
+            }
+            w[dd] = a;
+        }
+        *(half ? p1 : p0) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+}
+
 // Both operands' slices in one launch (small problems, one stream): blocks [0, gx*gy of A) encode A,
 // the rest B.  Saves a launch boundary and lets A's and B's tiles share the chip.
 struct EncOperand {
@@ -917,6 +1101,34 @@ void split_encode(const OperandDesc &d, bool is_A, size_t nvec, size_t len, cons
         else OZ2_LE(float, false, false);
     }
 #undef OZ2_LE
+}
+
+bool split_magnitudes(const OperandDesc &d, bool is_A, size_t nvec, size_t len, int16_t *sft0, int8_t *out,
+                      const Layout &L, void *scratch, size_t scratch_bytes, hipStream_t st) {
+    if (d.cplx || L.kblk == 0) return false;
+    const size_t vpad = round_up(is_A ? L.m_pad : L.n_pad, 64), ktiles = L.kblk / 64;
+    if (scratch_bytes < ktiles * vpad * sizeof(int2) + vpad * sizeof(int)) return false;
+    if (d.contig && vpad / 64 > 65536) return false;
+    int2 *ti = static_cast<int2 *>(scratch);
+    int *vexp = reinterpret_cast<int *>(ti + ktiles * vpad);
+    const int flags = d.contig ? ENC_KFIRST : 0;
+    const dim3 g1 = d.contig ? dim3((unsigned)ktiles, (unsigned)(vpad / 64)) : dim3((unsigned)(vpad / 64), (unsigned)ktiles);
+    const dim3 g2((unsigned)((nvec + 63) / 64)), g3((unsigned)((nvec + 31) / 32), (unsigned)((ktiles + 3) / 4));
+    if (g3.y > 65535) return false;
+    const bool nt = nvec * len * (d.dbl ? 8 : 4) >= NT_OPERAND_BYTES;
+#define OZ2_MG(R, C) do { \
+        const R *x = static_cast<const R *>(d.ptr); \
+        if (nt) launch(mag_tile_kernel<R, C, true>, g1, dim3(256), st, x, d.ld, nvec, len, out, L.ksteps, ti, vpad, flags); \
+        else launch(mag_tile_kernel<R, C, false>, g1, dim3(256), st, x, d.ld, nvec, len, out, L.ksteps, ti, vpad, flags); \
+        if (nvec) { \
+            launch(mag_vexp_kernel<R>, g2, dim3(256), st, nvec, ktiles, (const int2 *)ti, vpad, vexp, sft0); \
+            launch(mag_fixup_kernel<R, C>, g3, dim3(256), st, x, d.ld, nvec, len, out, L.ksteps, ktiles, \
+                   (const int2 *)ti, vpad, (const int *)vexp); \
+        } } while (0)
+    if (d.dbl) { if (d.contig) OZ2_MG(double, true); else OZ2_MG(double, false); }
+    else { if (d.contig) OZ2_MG(float, true); else OZ2_MG(float, false); }
+#undef OZ2_MG
+    return true;
 }
 
 bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,

@@ -769,3 +769,54 @@ def test_nonfinite_inputs(fast, dtype):
     B[7, 8] = -np.inf
     B[20, 30] = np.nan
     check_full(A, B, 12 if dtype == np.float64 else 7, fast=fast)
+
+
+def _magnitude_edge_rows(X, dtype):
+    """Rows of X (n_vec x k, k >= 256) that exercise the accurate mode's one-read magnitudes (split.hip
+    mag_tile_kernel / mag_fixup_kernel): tile amax below the vector amax by d = 1..7 and beyond, elements at and
+    across the subnormal boundary of the final scale, Inf / NaN in one tile, all-NaN, all-zero and -0.0 rows,
+    a 2^2000 (f64) dynamic range, magnitudes of exactly 64."""
+    dbl = dtype == np.float64
+    emin = -1022 if dbl else -126
+    X[1, :64] *= 1.0
+    X[1, 64:] *= 2.0 ** -17           # tiles 1.. : d = 17 (every nonzero byte -> 1)
+    X[2, 64:128] *= 0.3               # d = 1 or 2
+    X[2, 128:192] *= 2.0 ** -5        # d ~ 5
+    X[3, :] = 0.75
+    X[3, 100] = 2.0 ** (emin + 22)    # far from the boundary: exact path
+    X[4, :] = 0.75                    # amax 0.75: final scale 2^6
+    X[4, 150] = 2.0 ** (emin - 6)     # a subnormal input scaled exactly onto the least normal exponent: exact path
+    X[5, :] = 0.75
+    X[5, 70] = 2.0 ** (emin - 7)      # one below (subnormal under the final scale): recomputed from the operand
+    X[5, 71] = 2.0 ** (emin - 20)
+    X[6, 200] = np.inf
+    X[7, 90] = np.nan
+    X[8, :] = np.nan
+    X[9, :] = 0.0
+    X[10, :] = -0.0
+    X[10, 5] = 1.5
+    X[10, 130] = -0.0
+    if dbl:
+        X[11, :64] *= 1e300
+        X[11, 64:128] *= 1e-300
+    else:
+        X[11, :64] *= 1e30
+        X[11, 64:128] *= 1e-30
+    X[12, :] = 63.5                  # amax 63.5 -> sft0 = 0: bytes of 64
+    X[12, 64:] = 0.99                # tile amax below: d = 5
+    return X
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("opA,opB", [(0, 0), (1, 1)])
+def test_accurate_magnitudes_one_read_edges(dtype, opA, opB):
+    """Accurate mode's sft0 and magnitudes from one read of each operand (pass 1 scales by the tile amax, pass 2
+    rescales the bytes or recomputes the tile): shifts, slices, residues and C against the oracle at the edges of
+    that scheme, for strided (op N A, op T B) and contiguous (op T A, op N B) vectors."""
+    rng = np.random.default_rng(77)
+    m, n, k = 40, 36, 300
+    A = _magnitude_edge_rows(randmat_np(rng, m, k).astype(dtype), dtype)
+    Bt = _magnitude_edge_rows(randmat_np(rng, n, k).astype(dtype), dtype)  # rows of B^T = columns of B
+    A = np.asfortranarray(A.T) if opA else np.asfortranarray(A)
+    B = np.asfortranarray(Bt) if opB else np.asfortranarray(Bt.T)
+    check_full(A, B, 10 if dtype == np.float64 else 7, fast=False, opA=opA, opB=opB)

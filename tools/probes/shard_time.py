@@ -7,7 +7,9 @@ per link taken from the plan.  The critical path of a W-GPU run is the slowest r
 part of its receives does not overlap (the last stage's); the collectives (one all-gather of m + n int16)
 are left out.
 
-    python tools/probes/shard_time.py [size] [N] [W ...]     (defaults: 16384 14 2 4 8)"""
+    python tools/probes/shard_time.py [size] [N] [W ...]     (defaults: 16384 14 2 4 8)
+    SHARD_ORDER=columns: ShardPlan's column-block-major unit order (default moduli)"""
+import os
 import json
 import sys
 
@@ -55,7 +57,7 @@ def main():
         return best
 
     for W in Ws:
-        plan = GD.ShardPlan(m, n, N, W)
+        plan = GD.ShardPlan(m, n, N, W, order=os.environ.get("SHARD_ORDER", "moduli"))
         ranks = []
         for r in range(W):
             j0, j1 = plan.mods[r]
@@ -87,7 +89,7 @@ def main():
               f"last-stage receive {max(x['last_stage_recv_bytes'] for x in ranks) / 1e6:.0f} MB", flush=True)
         for x in ranks:
             print("   ", json.dumps(x), flush=True)
-    with open("gpurun_out/shard_time.json", "w") as f:
+    with open("gpurun_out/shard_time_%s.json" % os.environ.get("SHARD_ORDER", "moduli"), "w") as f:
         json.dump(out, f, indent=1)
 
 
