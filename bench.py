@@ -245,10 +245,9 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
     """SURVEY.md 8(e)'s partitions side by side, after the timed region, same operands (a few steps each):
     the default (modulus, column block) units with C gathered on the root; whole moduli per rank with the residue
     planes sent to the root and the root's CRT (variant (i)); row blocks of C, all moduli per rank, no exchange
-    (variant (ii), strong scaling); its 2-D form (output blocks on a near-square rank grid); and the communication
-    alone of the north-star's reduce of FP64 partial CRT sums (two m x n double accumulators to the root; not
-    bit-identical, so not built)."""
-    import torch.distributed as dist
+    (variant (ii), strong scaling); its 2-D form (output blocks on a near-square rank grid); and the north star's
+    reduce of FP64 partial CRT sums (gemm_moduli_reduce: two m x n double accumulators to the root; C within a
+    few ulp, not bit-identical)."""
     steps, warm = 3, 1
 
     def timed(fn):
@@ -295,9 +294,10 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
     out[f"output_blocks_{R}x{Q}_all_moduli"] = timed(blk)
     if fast and a1 > a0 and b1 > b0:
         del wb, Cb
-    part = torch.empty((2, n, m), dtype=torch.float64, device=A.device)
-    out["fp64_partial_sums_reduce_comm_only"] = timed(lambda: dist.reduce(part, dst=0))
-    del part
+    # the north star's partition as built (gemm_moduli_reduce): whole moduli per rank, partial FP64 CRT sums,
+    # one sum-reduce of the two m x n planes to the root, the root's finishing CRT (C within ulps, not bit-identical)
+    out["moduli_partial_sums_reduce"] = timed(
+        lambda: GD.gemm_moduli_reduce(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, ops=ops))
     torch.cuda.empty_cache()
     flops = 2.0 * m * n * k
     return {kk: ({"ms_per_step": round(v, 3), "tflops": round(flops / (v * 1e-3) / 1e12, 1)}

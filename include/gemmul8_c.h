@@ -124,6 +124,22 @@ int gemmul8_recombine_cols(void *stream, size_t m, size_t n, size_t k, unsigned 
                            int compute_type, const void *alpha, const void *beta, void *C, size_t ldc, void *work,
                            size_t col_begin, size_t col_end);
 
+/* --- partial CRT sums (the north star's "single RCCL reduce of partial FP64 accumulators") ------
+ * A rank holding the residue planes of moduli [mod_begin, mod_end) (gemmul8_split + gemmul8_products of that
+ * range, every shift in its workspace) writes per output element the partial CRT sums of its range into
+ * sums = column-major double [2][n][lds] (plane 0: C1 = sum hi_i r_i, plane 1: C2 = sum lo_i r_i; one-level
+ * moduli, N <= 7 or float output: C1 = sum NMi_i r_i, C2 = 0) -- inverse_scaling.hpp:35-62, 138-172
+ * restricted to the range.  The element-wise sums of all ranks' planes (an RCCL sum reduce) finish into C with
+ * gemmul8_crt_finish (sftA / sftB from `work`).  C1 is exact in any order; C2 is a rounded sum whose order the
+ * reduce changes, so C is within a few ulp of gemmul8_gemm's, not bit-identical.  Real outputs only
+ * (GEMMUL8_E_UNSUPPORTED for complex compute types). */
+int gemmul8_crt_partial(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c,
+                        int compute_type, const void *work, unsigned mod_begin, unsigned mod_end, double *sums,
+                        size_t lds);
+int gemmul8_crt_finish(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c,
+                       int compute_type, const void *alpha, const void *beta, void *C, size_t ldc, const void *work,
+                       const double *sums, size_t lds);
+
 /* --- instrumentation (used by bench.py / tests) --------------------------------------------- */
 /* When enabled, every gemmul8_gemm records HIP events between its phases on its stream; the
  * accumulated per-phase milliseconds and the call count are read (and reset) with

@@ -480,4 +480,136 @@ void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const i
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Partial CRT sums of a moduli range and the CRT finished from summed partials: the north star's
+// multi-GPU form (BASELINE.json: "a single RCCL reduce of partial FP64 accumulators"), gemmul8/dist.py
+// gemm_moduli_reduce.  A rank that holds the residue planes of moduli [j0, j1) writes per element
+// C1_g = sum hi_i r_i and C2_g = sum lo_i r_i over its range (the reference's fma chains of
+// inverse_scaling.hpp:138-172 restricted to it, i ascending; numM = 1: C_g = sum NMi_i r_i and C2_g = 0);
+// the ranks sum the two planes (RCCL reduce) and one finish applies the reference's tail: quot, the two-
+// step reduction, the scaling and the BLAS epilogue.  C1 is exact in any order (every term and partial sum
+// is a multiple of 2^tz below 2^(53+tz)), so C1 equals the single call's; C2 (the low words) and numM = 1
+// at N = 6, 7 are rounded sums whose order the reduce changes: C is then within a few ulp of the single
+// call's, not bit-identical (tests/test_gpu_phases.py measures it).  Real outputs only.
+struct CrtPartialArgs {
+    const uint8_t *R;
+    size_t planeR, ldr, m, n;
+    unsigned j0, j1;
+    int numM1;
+    double whi[OZ2_MAX_MODULI], wlo[OZ2_MAX_MODULI];
+    double *S;
+    size_t lds;
+};
+
+__global__ __launch_bounds__(256) void crt_partial_kernel(CrtPartialArgs a) {
+    const size_t r0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * CRT_ROWS;
+    if (r0 >= a.m) return;
+    const int nr = a.m - r0 >= CRT_ROWS ? CRT_ROWS : (int)(a.m - r0);
+    for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
+        double c1[CRT_ROWS] = {}, c2[CRT_ROWS] = {};
+        const uint8_t *q = a.R + col * a.ldr + r0;
+        for (unsigned j = a.j0; j < a.j1; ++j) {
+            uint64_t w = 0;
+            if (nr == CRT_ROWS) w = *reinterpret_cast<const uint64_t *>(q + j * a.planeR);
+            else
+                for (int e = 0; e < nr; ++e) w |= (uint64_t)q[j * a.planeR + e] << (8 * e);
+            const double hi = a.whi[j], lo = a.wlo[j];
+#pragma unroll
+            for (int e = 0; e < CRT_ROWS; ++e) {
+                const double r = (double)(uint8_t)(w >> (8 * e));
+                c1[e] = __builtin_fma(hi, r, c1[e]);
+                if (!a.numM1) c2[e] = __builtin_fma(lo, r, c2[e]);
+            }
+        }
+        double *s1 = a.S + col * a.lds + r0, *s2 = s1 + a.n * a.lds;
+        for (int e = 0; e < nr; ++e) {
+            s1[e] = c1[e];
+            s2[e] = c2[e];
+        }
+    }
+}
+
+struct CrtFinishArgs {
+    const double *S;
+    size_t lds, m, n;
+    const int16_t *sftA, *sftB;
+    void *C;
+    size_t ldc;
+    int f32, numM1, ref_epi;
+    double invM, M1, M2, ar, br;
+};
+
+__global__ __launch_bounds__(256) void crt_finish_kernel(CrtFinishArgs a) {
+    const size_t row = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (row >= a.m) return;
+    const int sA = a.sftA[row];
+    for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
+        const double C1 = a.S[col * a.lds + row], C2 = a.S[(a.n + col) * a.lds + row];
+        double v;
+        if (a.numM1) {
+            const double quot = -__builtin_rint(C1 * a.invM);
+            v = __builtin_fma(quot, a.M1, C1);
+        } else {
+            const double quot = -__builtin_rint(__builtin_fma(C1, a.invM, C2 * a.invM));
+            const double t1 = __builtin_fma(quot, a.M1, C1) + C2;
+            v = __builtin_fma(quot, a.M2, t1);
+        }
+        v = scalbn(v, sA + (int)a.sftB[col]);
+        const bool zero_beta = a.br == 0.0 && !(a.ref_epi && a.ar != 1.0);
+        if (a.f32) {
+            float *C = static_cast<float *>(a.C) + col * a.ldc + row;
+            const float x = __double2float_rn(v);
+            *C = (a.ar == 1.0 && a.br == 0.0) ? x : epi_f(x, zero_beta ? 0.f : *C, (float)a.ar, (float)a.br, a.ref_epi != 0);
+        } else {
+            double *C = static_cast<double *>(a.C) + col * a.ldc + row;
+            *C = (a.ar == 1.0 && a.br == 0.0) ? v : epi_d(v, zero_beta ? 0.0 : *C, a.ar, a.br, a.ref_epi != 0, a.numM1 != 0);
+        }
+    }
+}
+
+void crt_partial(const uint8_t *R, const Layout &L, unsigned N, bool numM1, unsigned j0, unsigned j1, double *S,
+                 size_t lds, hipStream_t st) {
+    CrtPartialArgs a{};
+    a.R = R;
+    a.planeR = L.planeR;
+    a.ldr = L.ldr;
+    a.m = L.m;
+    a.n = L.n;
+    a.j0 = j0;
+    a.j1 = j1;
+    a.numM1 = numM1 ? 1 : 0;
+    for (unsigned j = 0; j < N; ++j) {
+        a.whi[j] = numM1 ? oz2_NMi_1[N - 2][j] : oz2_NMi_2[N - 8][j][0];
+        a.wlo[j] = numM1 ? 0.0 : oz2_NMi_2[N - 8][j][1];
+    }
+    a.S = S;
+    a.lds = lds;
+    const dim3 grid((unsigned)((L.m + 256 * CRT_ROWS - 1) / (256 * CRT_ROWS)), (unsigned)(L.n < 65535 ? L.n : 65535));
+    launch(crt_partial_kernel, grid, dim3(256), st, a);
+}
+
+void crt_finish(const double *S, size_t lds, const Layout &L, unsigned N, bool numM1, const int16_t *sftA,
+                const int16_t *sftB, bool f32, const void *alpha, const void *beta, void *C, size_t ldc,
+                hipStream_t st, int ref_epi) {
+    CrtFinishArgs a{};
+    a.S = S;
+    a.lds = lds;
+    a.m = L.m;
+    a.n = L.n;
+    a.sftA = sftA;
+    a.sftB = sftB;
+    a.C = C;
+    a.ldc = ldc;
+    a.f32 = f32 ? 1 : 0;
+    a.numM1 = numM1 ? 1 : 0;
+    a.ref_epi = ref_epi;
+    a.invM = oz2_invM[N - 2];
+    a.M1 = oz2_M_hi[N - 2];
+    a.M2 = oz2_M_lo[N - 2];
+    a.ar = f32 ? (double)*(const float *)alpha : *(const double *)alpha;
+    a.br = f32 ? (double)*(const float *)beta : *(const double *)beta;
+    const dim3 grid((unsigned)((L.m + 255) / 256), (unsigned)(L.n < 65535 ? L.n : 65535));
+    launch(crt_finish_kernel, grid, dim3(256), st, a);
+}
+
 }  // namespace oz2

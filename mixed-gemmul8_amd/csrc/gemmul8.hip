@@ -686,6 +686,46 @@ int gemmul8_recombine_cols(void *stream, size_t m, size_t n, size_t k, unsigned 
     return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
 }
 
+// partial CRT sums / finish (the north star's reduce of FP64 partial accumulators; include/gemmul8_c.h)
+static int crt_parts_check(size_t m, size_t n, unsigned num_moduli, int type_c, int compute_type, size_t lds) {
+    if (num_moduli < 2 || num_moduli > 20) return GEMMUL8_E_MODULI;
+    if (compute_type != GEMMUL8_REAL_DEFAULT) return GEMMUL8_E_UNSUPPORTED;
+    if (type_c != GEMMUL8_R_64F && type_c != GEMMUL8_R_32F) return GEMMUL8_E_TYPES;
+    if (lds < m) return GEMMUL8_E_SIZE;
+    (void)n;
+    return GEMMUL8_OK;
+}
+
+int gemmul8_crt_partial(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c,
+                        int compute_type, const void *work, unsigned mod_begin, unsigned mod_end, double *sums,
+                        size_t lds) {
+    const int rc = crt_parts_check(m, n, num_moduli, type_c, compute_type, lds);
+    if (rc != GEMMUL8_OK) return rc;
+    if (mod_begin > mod_end || mod_end > num_moduli) return GEMMUL8_E_MODULI;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
+    const oz2::Views v = oz2::views(const_cast<void *>(work), m, n, k, num_moduli, false);
+    const oz2::CrtParams CP = oz2::make_crt_params(num_moduli, type_c == GEMMUL8_R_32F);
+    oz2::crt_partial(v.R, v.L, num_moduli, CP.numM1 != 0, mod_begin, mod_end, sums, lds,
+                     static_cast<hipStream_t>(stream));
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_crt_finish(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c,
+                       int compute_type, const void *alpha, const void *beta, void *C, size_t ldc, const void *work,
+                       const double *sums, size_t lds) {
+    const int rc = crt_parts_check(m, n, num_moduli, type_c, compute_type, lds);
+    if (rc != GEMMUL8_OK) return rc;
+    if (ldc < m) return GEMMUL8_E_SIZE;
+    if (m == 0 || n == 0) return GEMMUL8_OK;
+    oz2::clear_stale_error();
+    const oz2::Views v = oz2::views(const_cast<void *>(work), m, n, k, num_moduli, false);
+    const oz2::CrtParams CP = oz2::make_crt_params(num_moduli, type_c == GEMMUL8_R_32F);
+    oz2::crt_finish(sums, lds, v.L, num_moduli, CP.numM1 != 0, v.sftA, v.sftB, type_c == GEMMUL8_R_32F, alpha, beta,
+                    C, ldc, static_cast<hipStream_t>(stream), oz2::g_epilogue_mode.load(std::memory_order_relaxed));
+    return oz2::launch_ok() ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
 int gemmul8_shard_stats(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
                         int type_c, const void *A, size_t lda, const void *B, size_t ldb, unsigned num_moduli,
                         int fastmode, void *work, int compute_type, size_t row_begin, size_t row_end,

@@ -123,4 +123,12 @@ enum class OutType : int { F64 = 0, F32 = 1, C64 = 2, C32 = 3 };
 void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const int16_t *sftB, const CrtParams &CP,
                  OutType ot, const void *alpha, const void *beta, void *C, size_t ldc, hipStream_t st, int ref_epi);
 
+// partial CRT sums of moduli [j0, j1) into S ([2][n][lds]: C1 then C2) and the CRT finished from summed
+// partials (real outputs; gemmul8_crt_partial / gemmul8_crt_finish)
+void crt_partial(const uint8_t *R, const Layout &L, unsigned N, bool numM1, unsigned j0, unsigned j1, double *S,
+                 size_t lds, hipStream_t st);
+void crt_finish(const double *S, size_t lds, const Layout &L, unsigned N, bool numM1, const int16_t *sftA,
+                const int16_t *sftB, bool f32, const void *alpha, const void *beta, void *C, size_t ldc,
+                hipStream_t st, int ref_epi);
+
 }  // namespace oz2

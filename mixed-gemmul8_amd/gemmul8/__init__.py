@@ -48,6 +48,8 @@ def _load():
     lib.gemmul8_shard_bound.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, sz, p, sz, u, p, i, sz, sz]
     lib.gemmul8_products_cols.argtypes = [p, sz, sz, sz, u, i, p, u, u, sz, sz]
     lib.gemmul8_recombine_cols.argtypes = [p, sz, sz, sz, u, i, i, p, p, p, sz, p, sz, sz]
+    lib.gemmul8_crt_partial.argtypes = [p, sz, sz, sz, u, i, i, p, u, u, p, sz]
+    lib.gemmul8_crt_finish.argtypes = [p, sz, sz, sz, u, i, i, p, p, p, sz, p, p, sz]
     lib.gemmul8_work_size_lowmem.restype = sz
     lib.gemmul8_work_size_lowmem.argtypes = [sz, sz, sz, u, i, u]
     lib.gemmul8_gemm_lowmem.restype = i
@@ -211,6 +213,22 @@ def recombine(m, n, k, num_moduli, alpha, beta, C, ldc, work, computeType=REAL_D
     else:
         _check(lib.gemmul8_recombine_cols(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], computeType, al.ptr,
                                           be.ptr, C.data_ptr(), ldc, work.data_ptr(), cols[0], cols[1]))
+
+
+def crt_partial(m, n, k, num_moduli, out_dtype, work, mod_begin, mod_end, sums, stream=None):
+    """Partial CRT sums of moduli [mod_begin, mod_end) into `sums` (float64 tensor (2, n, m): C1 then C2,
+    column-major planes; real outputs).  The element-wise sums of the partials of a moduli partition
+    finish with crt_finish (include/gemmul8_c.h: C1 exact, C2 rounded in the summation order)."""
+    assert sums.dtype == torch.float64 and sums.numel() >= 2 * n * m
+    _check(lib.gemmul8_crt_partial(_stream(stream), m, n, k, num_moduli, _DTYPE[out_dtype], REAL_DEFAULT,
+                                   work.data_ptr(), mod_begin, mod_end, sums.data_ptr(), m))
+
+
+def crt_finish(m, n, k, num_moduli, alpha, beta, C, ldc, work, sums, stream=None):
+    """C = alpha * CRT(summed partials) scaled by the workspace's shifts + beta * C (real outputs)."""
+    al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
+    _check(lib.gemmul8_crt_finish(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], REAL_DEFAULT, al.ptr, be.ptr,
+                                  C.data_ptr(), ldc, work.data_ptr(), sums.data_ptr(), m))
 
 
 def residue_planes(work, m, n, k, num_moduli, mod_begin=0, mod_end=None, computeType=REAL_DEFAULT):

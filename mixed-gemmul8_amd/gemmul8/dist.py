@@ -66,11 +66,12 @@ import torch
 import torch.distributed as dist
 
 from . import (OP_N, OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, gemm, layout, split, split_bound,
-               products, recombine, shard_stats, shard_bound)
+               products, recombine, shard_stats, shard_bound, crt_partial, crt_finish)
 
 __all__ = ["OP_N", "OP_T", "REAL_DEFAULT", "COMPLEX_BIG_MATRIX_ENCODE", "ShardPlan", "HipShardOps", "HipOps", "blocks",
            "moduli_partition", "row_partition", "gemm_moduli", "gemm_moduli_planes_to_root", "matmul_moduli",
-           "matmul_rows", "release_workspaces", "side_stream_enabled", "StageWatchdog", "progress"]
+           "matmul_rows", "release_workspaces", "side_stream_enabled", "StageWatchdog", "progress",
+           "gemm_moduli_reduce"]
 
 TILE = 256  # product tile edge: column blocks of the product units start at multiples of it
 WORKSPACE_CACHE = 2  # workspaces (shapes) kept per native ops object
@@ -348,6 +349,22 @@ class HipShardOps:
             recombine(m, st["n"], st["k"], st["N"], 1.0, 0.0, Cb, m, st["work"], st["ct"], cols=(c0, c1))
         return Cb
 
+    def partial(self, st, j0, j1):
+        """partial CRT sums (C1, C2) of moduli [j0, j1) as a float64 (2, n, m) tensor (zeros for an empty range)"""
+        m, n = st["m"], st["n"]
+        S = torch.zeros((2, n, m), dtype=torch.float64, device=st["dev"]) if j1 <= j0 else \
+            torch.empty((2, n, m), dtype=torch.float64, device=st["dev"])
+        if j1 > j0:
+            crt_partial(m, n, st["k"], st["N"], st["dtype"], st["work"], j0, j1, S)
+        return S
+
+    def finish(self, st, S):
+        """C (an (n, m) tensor) from the summed partial CRT sums and the workspace's shifts"""
+        m, n = st["m"], st["n"]
+        C = torch.empty((n, m), dtype=st["dtype"], device=st["dev"])
+        crt_finish(m, n, st["k"], st["N"], 1.0, 0.0, C, m, st["work"], S)
+        return C
+
     def side_stream(self):
         """a stream with no work of this call on it (receive-only transfer stages are posted from it)"""
         dev = torch.cuda.current_device()
@@ -580,6 +597,45 @@ def gemm_moduli_planes_to_root(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14,
     for q in reqs:
         q.wait()
     return ops.recombine(st, 0, n)
+
+
+def gemm_moduli_reduce(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None, group=None,
+                       root=0, ops=None):
+    """The north star's partition (BASELINE.json): whole moduli per rank (moduli_partition: 14 over 8 ranks
+    2,2,2,2,2,2,1,1), every rank its own shifts, residue planes and partial CRT sums (C1, C2) of its moduli, ONE
+    RCCL sum-reduce of the two FP64 m x n planes to the root, and the root's finishing CRT (include/gemmul8_c.h
+    gemmul8_crt_partial / gemmul8_crt_finish).  Real outputs, alpha = 1, beta = 0.  C1 sums exactly in any order;
+    C2 is a rounded sum whose order the reduce changes, so C is within a few ulp of the single call's but not
+    bit-identical, and the reduce moves 16 B per element per rank (4.3 GB at cfg3) against gemm_moduli's residue
+    exchange (N m n / W bytes received per rank, 0.47 GB).  Kept for comparison (bench.py times it).  Returns C
+    (n, m) on the root, None elsewhere."""
+    ops = ops or _shard_ops()
+    out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
+    rank, world = _group_info(group)
+    host_sync = dist.get_backend(group) != "nccl"
+    j0, j1 = moduli_partition(num_moduli, world)[rank]
+    st = ops.prepare(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, out_dtype, REAL_DEFAULT)
+    with _PROGRESS_LOCK:
+        _PROGRESS["call"] += 1
+    progress("reduce: shifts / encode", f"moduli [{j0}, {j1})")
+    ops.stats(st, (0, m), (0, n))
+    if not fastmode:
+        ops.bound(st, (0, n))
+    if j1 > j0 or not fastmode:
+        ops.encode(st, j0, j1)
+    if j1 > j0:
+        ops.products(st, j0, j1, 0, n)
+    S = ops.partial(st, j0, j1)
+    if host_sync:
+        ops.sync()
+    progress("reduce: sum of partial CRT sums", f"2 x {m} x {n} f64 to rank {root}")
+    dist.reduce(S, dst=_global(group, root), op=dist.ReduceOp.SUM, group=group)
+    if rank != root:
+        progress("done")
+        return None
+    C = ops.finish(st, S)
+    progress("done")
+    return C
 
 
 def matmul_moduli(A, B, num_moduli=14, fastmode=True, out_dtype=None, group=None, gather=True, root=0, ops=None,

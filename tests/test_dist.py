@@ -54,6 +54,36 @@ class OracleOps:
         pass
 
 
+def _fma1(a, b, c):
+    from fractions import Fraction
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def fma(a, b, c):
+    """element-wise correctly rounded a * b + c (the finishing CRT cancels q * M against C1: a separately
+    rounded product would lose it)"""
+    return np.frompyfunc(_fma1, 3, 1)(*np.broadcast_arrays(np.float64(a), np.float64(b), np.float64(c))).astype(np.float64)
+
+
+def crt_tables():
+    """the CRT constants of mixed-gemmul8_amd/csrc/oz2_tables.inc (hex floats) as numpy arrays"""
+    import re
+    txt = open(os.path.join(ROOT, "mixed-gemmul8_amd", "csrc", "oz2_tables.inc")).read()
+
+    def arr(name):
+        body = re.search(r"\b" + name + r"\[[^=]*=\s*\{(.*?)\};", txt, re.S).group(1)
+        return [float.fromhex(x) if "0x" in x else float(x) for x in re.findall(r"-?0x[0-9a-fA-Fp.+-]+|-?\d+\.\d+", body)]
+    numM = [int(x) for x in re.search(r"oz2_numM\[19\] = \{(.*?)\}", txt).group(1).split(",")]
+    nmi1 = np.zeros((19, 20))
+    body1 = re.search(r"oz2_NMi_1\[19\]\[20\] = \{(.*?)\};", txt, re.S).group(1)
+    for r, row in enumerate(re.findall(r"\{([^{}]*)\}", body1)):
+        vals = [float.fromhex(x) for x in re.findall(r"-?0x[0-9a-fA-Fp.+-]+", row)]
+        nmi1[r, :len(vals)] = vals
+    nmi2 = np.array(arr("oz2_NMi_2")).reshape(13, 20, 2)
+    return {"numM": numM, "NMi_1": nmi1, "NMi_2": nmi2, "invM": np.array(arr("oz2_invM")),
+            "M_hi": np.array(arr("oz2_M_hi")), "M_lo": np.array(arr("oz2_M_lo"))}
+
+
 class OracleShardOps:
     """CPU stand-in for gemmul8.dist.HipShardOps (tests only).  The shifts and residues are computed
     in full by the oracle but published only for this rank's rows / columns / units, so the result
@@ -74,7 +104,7 @@ class OracleShardOps:
         npt = torch.empty((), dtype=out_dtype).numpy().dtype
         # fast mode: the published shifts are what the ranks gather; accurate mode gathers sft0 (stood in for by
         # the same values here) and derives the final shifts in encode (the native finalize), on every rank
-        return {"sA": sA, "sB": sB, "full": full, "R": torch.zeros(full.shape, dtype=torch.uint8), "fast": fast,
+        return {"sA": sA, "sB": sB, "full": full, "R": torch.zeros(full.shape, dtype=torch.uint8), "fast": fast, "N": N,
                 "pA": torch.full((m,), self.SENTINEL, dtype=torch.int16),
                 "pB": torch.full((n,), self.SENTINEL, dtype=torch.int16),
                 "gA": torch.full((m,), self.SENTINEL, dtype=torch.int16),
@@ -103,6 +133,33 @@ class OracleShardOps:
     def chunks(self, st, j, c0, c1):
         return [st["R"][j, c0:c1].view(-1)]
 
+    # the reduce partition (gemm_moduli_reduce): numpy restatement of gemmul8_crt_partial / _finish (mul + add
+    # where the library fuses: the C2 sums differ in rounding anyway, the tests compare within ulps)
+    def partial(self, st, j0, j1):
+        T, N = crt_tables(), st["N"]
+        numM1 = T["numM"][N - 2] == 1 or st["dtype"] == np.float32
+        n, m = st["full"].shape[1:]
+        C1, C2 = np.zeros((n, m)), np.zeros((n, m))
+        for j in range(j0, j1):
+            r = st["R"][j].numpy().astype(np.float64)
+            C1 = (T["NMi_1"][N - 2][j] if numM1 else T["NMi_2"][N - 8][j][0]) * r + C1
+            if not numM1:
+                C2 = T["NMi_2"][N - 8][j][1] * r + C2
+        return torch.from_numpy(np.stack([C1, C2]))
+
+    def finish(self, st, S):
+        T, N = crt_tables(), st["N"]
+        numM1 = T["numM"][N - 2] == 1 or st["dtype"] == np.float32
+        C1, C2 = S[0].numpy(), S[1].numpy()
+        invM, M1, M2 = T["invM"][N - 2], T["M_hi"][N - 2], T["M_lo"][N - 2]
+        if numM1:
+            v = fma(-np.rint(C1 * invM), M1, C1)
+        else:
+            q = -np.rint(fma(C1, invM, C2 * invM))
+            v = fma(q, M2, fma(q, M1, C1) + C2)
+        sh = st["pB"].numpy().astype(np.int64)[:, None] + st["pA"].numpy().astype(np.int64)[None, :]
+        return torch.from_numpy(np.ldexp(v, sh).astype(st["dtype"]))
+
     def recombine(self, st, c0, c1):
         C = self.O.crt(np.ascontiguousarray(st["R"][:, c0:c1].numpy()), st["pA"].numpy(),
                        np.ascontiguousarray(st["pB"][c0:c1].numpy()), st["dtype"])
@@ -130,6 +187,14 @@ def _worker(rank, world, port, case, outdir):
         Cb = GD.matmul_moduli(torch.from_numpy(A), torch.from_numpy(B), N, fast, gather=False, ops=OracleShardOps(),
                               align=16, order=order)
         np.save(os.path.join(outdir, f"block{rank}.npy"), Cb.contiguous().numpy())
+        # the north star's partition: whole moduli per rank, partial CRT sums reduced to the root
+        if not np.iscomplexobj(A):  # (real outputs only)
+            Cr = GD.gemm_moduli_reduce(1, 1, m, n, k, torch.from_numpy(A), k, torch.from_numpy(B), n, N, fast,
+                                       ops=OracleShardOps())
+            if rank == 0:
+                np.save(os.path.join(outdir, "reduce.npy"), Cr.t().contiguous().numpy())
+            else:
+                assert Cr is None
         # SURVEY 8(e) variant (i): whole moduli per rank, planes gathered on the root
         Cp = GD.gemm_moduli_planes_to_root(1, 1, m, n, k, torch.from_numpy(A), k, torch.from_numpy(B), n, N, fast,
                                            ops=OracleShardOps())
@@ -178,6 +243,13 @@ def test_sharded_equals_single_call(tmp_path, world, case):
         got = np.load(tmp_path / f"{name}.npy")
         assert got.shape == C.shape
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C).view(np.uint8)), name
+    # the reduce of partial sums: within a few ulp of the single call (C2's summation order differs)
+    if not np.iscomplexobj(A):
+        got = np.load(tmp_path / "reduce.npy")
+        assert got.shape == C.shape and np.isfinite(got).all()
+        # (float output: a C sum a few ulp off can round to the neighbouring float)
+        tol = 2.0 ** (-19 if got.dtype == np.float32 else -40)
+        assert np.max(np.abs(got - C)) <= tol * np.max(np.abs(C)), np.max(np.abs(got - C))
     from gemmul8.dist import ShardPlan
     for r, (c0, c1) in enumerate(ShardPlan(m, n, N, world, 16, case[6] if len(case) > 6 else "moduli").cols):
         got = np.load(tmp_path / f"block{r}.npy")

@@ -70,6 +70,53 @@ def test_moduli_ranges_compose(m, n, k, N, fast, dt):
     assert _same(Ct.t(), ref)
 
 
+@pytest.mark.parametrize("m,n,k,N,fast,dt", [
+    (300, 260, 500, 14, True, "f64"), (257, 190, 333, 20, False, "f64"), (200, 128, 256, 6, True, "f64"),
+    (210, 140, 300, 8, True, "f64"), (200, 128, 256, 7, True, "f32"), (180, 100, 200, 12, False, "f32"),
+])
+def test_partial_crt_sums(m, n, k, N, fast, dt):
+    """gemmul8_crt_partial / _finish (the north star's reduce of FP64 partial CRT sums, gemm_moduli_reduce):
+    over the full moduli range the finish reproduces the single call bit for bit; over a partition, the summed
+    C1 planes equal the full range's exactly and C is within a few ulp (C2's summation order differs)."""
+    import torch
+    import gemmul8 as G
+    tdt = torch.float64 if dt == "f64" else torch.float32
+    A, B = _rand(m, k, 11, tdt), _rand(k, n, 12, tdt)
+    ref = _single(A, B, N, fast, tdt)
+    work = G.alloc_work(m, n, k, N)
+    G.split(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, fast, work, tdt)
+    G.products(m, n, k, N, work)
+    full = torch.empty((2, n, m), dtype=torch.float64, device="cuda")
+    G.crt_partial(m, n, k, N, tdt, work, 0, N, full)
+    Ct = torch.empty((n, m), dtype=tdt, device="cuda")
+    G.crt_finish(m, n, k, N, 1.0, 0.0, Ct, m, work, full)
+    torch.cuda.synchronize()
+    assert _same(Ct.t(), ref)
+    parts = [(0, 1), (1, N // 2), (N // 2, N - 1), (N - 1, N)]
+    S = torch.zeros((2, n, m), dtype=torch.float64, device="cuda")
+    for j0, j1 in parts:
+        Sp = torch.empty_like(S)
+        G.crt_partial(m, n, k, N, tdt, work, j0, j1, Sp)
+        S += Sp
+    G.crt_finish(m, n, k, N, 1.0, 0.0, Ct, m, work, S)
+    torch.cuda.synchronize()
+    numM2 = N >= 8 and dt == "f64"
+    if numM2 or N <= 5:  # exact C1 (and numM = 1 with exact sums)
+        assert torch.equal(S[0], full[0])
+    # one-level moduli at N = 6, 7 sum C = sum NMi r_i beyond 2^53 (rounded in any order: the single call's own
+    # error there is of that size); two-level: only the low words' sum is reordered; float: the output rounding
+    tol = 2.0 ** (-19 if dt == "f32" else -40 if (numM2 or N <= 5) else -26)
+    err = (Ct.t().double() - ref.double()).abs().max().item()
+    assert err <= tol * ref.double().abs().max().item(), err
+    # alpha / beta through the same epilogue as the single call
+    C0 = _rand(m, n, 13, tdt)
+    Cab, Cref = C0.t().contiguous().clone(), C0.t().contiguous().clone()
+    G.crt_finish(m, n, k, N, 2.5, -0.5, Cab, m, work, full)
+    G.recombine(m, n, k, N, 2.5, -0.5, Cref, m, work)
+    torch.cuda.synchronize()
+    assert _same(Cab, Cref)
+
+
 @pytest.mark.parametrize("fast", [True, False])
 def test_moduli_ranges_compose_complex_karatsuba(fast):
     """complex at a shape where the size rule runs Karatsuba sub-products (k >= 3072, m >= 1024): split /
@@ -137,6 +184,7 @@ def _port():
 def test_dist_one_rank_rccl():
     import torch
     import torch.distributed as dist
+    import gemmul8 as G
     from gemmul8 import dist as GD
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
@@ -157,6 +205,11 @@ def test_dist_one_rank_rccl():
         assert _same(GD.matmul_moduli(A2, B2, N, False), _single(A2, B2, N, False, torch.float64))
         assert _same(GD.matmul_moduli(A, B, N, False), refa)
         assert _same(GD.matmul_moduli(A, B, N, False, order="columns"), refa)
+        # the north star's reduce of partial CRT sums, one rank: the whole moduli range, so the same bits
+        Cr = GD.gemm_moduli_reduce(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True)
+        assert _same(Cr.t(), ref)
+        Cr = GD.gemm_moduli_reduce(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, False)
+        assert _same(Cr.t(), refa)
         os.environ["GEMMUL8_DIST_SIDE_STREAM"] = "0"
         try:
             assert _same(GD.matmul_moduli(A2, B2, N, True), _single(A2, B2, N, True, torch.float64))
