@@ -241,7 +241,7 @@ def make_operands(kind, m, n, k, seed_a, dev):
     return G.randmat(m, k, torch.float64, 0.5, seed_a, dev), G.randmat(k, n, tb, 0.5, 123456, dev), torch.float64
 
 
-def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
+def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lambda name: None):
     """SURVEY.md 8(e)'s partitions side by side, after the timed region, same operands (a few steps each):
     the default (modulus, column block) units with C gathered on the root; whole moduli per rank with the residue
     planes sent to the root and the root's CRT (variant (i)); row blocks of C, all moduli per rank, no exchange
@@ -250,7 +250,12 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
     few ulp, not bit-identical)."""
     steps, warm = 3, 1
 
-    def timed(fn):
+    stall = os.environ.get("GEMMUL8_BENCH_REHEARSE_STALL")  # rehearsal of the fail-soft path (DESIGN.md 8)
+
+    def timed(name, fn):
+        arm(name)
+        if stall == name and rank == world - 1:
+            time.sleep(1e9)  # the last rank never arrives: the others' collectives of this variant wait on it
         try:
             for _ in range(warm):
                 fn()
@@ -264,9 +269,9 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
         return reduce_max(time.perf_counter() - t0, world) / steps * 1e3
 
     out = {}
-    out["moduli_columns_gathered"] = timed(
+    out["moduli_columns_gathered"] = timed("moduli_columns_gathered",
         lambda: GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, gather=True, ops=ops))
-    out["moduli_whole_planes_to_root"] = timed(
+    out["moduli_whole_planes_to_root"] = timed("moduli_whole_planes_to_root",
         lambda: GD.gemm_moduli_planes_to_root(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, ops=ops))
     r0, r1 = GD.blocks(m, world)[rank]
     if r1 > r0:
@@ -276,7 +281,7 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
         rows = lambda: G.gemm(G.OP_N, G.OP_N, r1 - r0, n, k, 1.0, Ar, m, B, k, 0.0, Cr, r1 - r0, N, fast, wr)
     else:
         rows = lambda: None
-    out["row_blocks_all_moduli"] = timed(rows)
+    out["row_blocks_all_moduli"] = timed("row_blocks_all_moduli", rows)
     if r1 > r0:
         del wr, Cr
     # 2-D output blocks, all moduli per rank (grid R x Q = W with R, Q closest to sqrt(W)): each rank reads and
@@ -291,12 +296,12 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops):
         blk = lambda: G.gemm(G.OP_N, G.OP_N, a1 - a0, b1 - b0, k, 1.0, Ab, m, Bb, k, 0.0, Cb, a1 - a0, N, fast, wb)
     else:
         blk = lambda: None
-    out[f"output_blocks_{R}x{Q}_all_moduli"] = timed(blk)
+    out[f"output_blocks_{R}x{Q}_all_moduli"] = timed(f"output_blocks_{R}x{Q}_all_moduli", blk)
     if fast and a1 > a0 and b1 > b0:
         del wb, Cb
     # the north star's partition as built (gemm_moduli_reduce): whole moduli per rank, partial FP64 CRT sums,
     # one sum-reduce of the two m x n planes to the root, the root's finishing CRT (C within ulps, not bit-identical)
-    out["moduli_partial_sums_reduce"] = timed(
+    out["moduli_partial_sums_reduce"] = timed("moduli_partial_sums_reduce",
         lambda: GD.gemm_moduli_reduce(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, ops=ops))
     torch.cuda.empty_cache()
     flops = 2.0 * m * n * k
@@ -384,7 +389,7 @@ def main():
     if world > 1:
         # fail fast: a phase that outlives its limit ends this rank with the stage and peers it was at
         wd = GD.StageWatchdog(float(os.environ.get("GEMMUL8_DIST_WATCHDOG_S", "240")), rank)
-    arm = (lambda ph: wd.arm(ph)) if wd else (lambda ph: None)
+    arm = (lambda ph, on_fire=None: wd.arm(ph, on_fire)) if wd else (lambda ph, on_fire=None: None)
 
     W = select_workload(args, world)
     wl_name, wl, m, N, fast, kind, custom = W["name"], W["wl"], W["m"], W["N"], W["fast"], W["kind"], W["custom"]
@@ -477,14 +482,66 @@ def main():
                                  "frac": round(work_alg["int8_ops"] / (world * INT8_PEAK_TOPS * 1e12 * ms_per_step * 1e-3), 4),
                                  "formula": "sum over ranks of int8 ops / (W * P_int8 * t_step)"}
 
-    if sharded and kind == "d" and not args.no_variants:
-        arm("variants")
-        extra["variants"] = time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops)
+    if not sharded and not rows_accurate:
+        extra["phase_ms"] = {"scaling": round(avg[0], 4), "int8_products": round(avg[1], 4),
+                             "inverse_scaling": round(avg[3], 4)}
+        roofline["composite"] = composite_roofline(work_alg, ms_per_step, extra["phase_ms"])
+    elif sharded:
+        roofline["composite"] = composite_roofline(work_alg, ms_per_step, None, world)
+    report = {"cpu": None}
+
+    def line(incomplete=None):
+        """rank 0's JSON line from what has been measured so far"""
+        workload, metric = labels(W)
+        out = {
+            "metric": metric,
+            "value": round(value, 3),
+            "unit": "TFLOP/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "strong" if sharded else ("weak" if world > 1 else "single"),
+            "vs_baseline": round(value / world / GH200_PUBLISHED_TFLOPS, 3) if (wl_name == "cfg2" and not custom) else None,
+            "vs_baseline_ref": "GH200 published OS2-fast-14 8192 (72.13 TFLOP/s, BASELINE.md); per-GPU ratio",
+            "dtype": "i8",
+            "io_dtype": {"d": "f64", "dfd": "f64*f32->f64", "z": "c128"}[kind],
+            "data": "synthetic: hiprand XORWOW (U-0.5)*exp(0.5*N(0,1)), seed 123456, A == B as in the reference "
+                    "driver" + (" (row partition: rank r's A seed 123456+r)" if (world > 1 and not sharded) else ""),
+            "config": {"workload": workload, "m": m, "n": n, "k": k, "num_moduli": N, "fastmode": fast,
+                       "parallelism": (("moduli x column blocks" if sharded else "rows") + f" x{world}")
+                       if world > 1 else "single",
+                       "world_size": world, "backend": backend or "none",
+                       "output": ("C gathered on rank 0" if args.gather else "C distributed by column blocks")
+                       if sharded else "C on each rank"},
+            "roofline": roofline,
+            "cpu_baseline": report["cpu"],
+        }
+        if sharded:
+            out["config"]["unit_order"] = args.order
+            out["config"]["dist_side_stream"] = GD.side_stream_enabled() and backend == "nccl"
+            out["config"]["dist_timeout_s"] = float(os.environ.get("GEMMUL8_DIST_TIMEOUT", "300"))
+        out.update(dict(extra))
+        if incomplete:
+            # a phase after the timed region outlived the watchdog: the timed steps above stand, the fields
+            # that phase and the later ones would have added are missing
+            out["incomplete"] = incomplete
+        return out
+
+    # the phases after the timed region are optional: if one of them gets stuck (a collective of a variant
+    # whose peer failed, say), rank 0 prints the line measured so far and every rank exits with status 0
+    if rank == 0:
+        def soft(msg):
+            print(json.dumps(line(msg)), flush=True)
+    else:
+        def soft(msg):
+            pass
 
     # accuracy against a double-double reference (testing/eval.hpp semantics); sharded: each rank checks
     # its own output columns, the max is combined
     if not args.no_accuracy and not cplx and kind == "d":
-        arm("accuracy")
+        arm("accuracy", soft)
         Cout = step()
         torch.cuda.synchronize()
         if sharded:
@@ -519,7 +576,7 @@ def main():
     if sharded and not args.no_single_gpu:
         # the same call on ONE GPU (rank 0, after the timed region; the other ranks wait at the barrier): the
         # strong-scaling efficiency of this line is single_gpu_ms / (W * ms_per_step)
-        arm("single-GPU baseline")
+        arm("single-GPU baseline", soft)
         GD.release_workspaces(ops)
         torch.cuda.empty_cache()
         if rank == 0:
@@ -543,8 +600,13 @@ def main():
             torch.cuda.empty_cache()
         barrier(world)
 
+    if sharded and kind == "d" and not args.no_variants:
+        # last of the collective phases: each variant is a phase of its own for the watchdog
+        extra["variants"] = time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops,
+                                          arm=lambda name: arm(f"variants: {name}", soft))
+
     if rank == 0:
-        arm("report")
+        arm("report", soft)
         # measured live after the timed region: the same MFMA alone on uniformly random operand bytes
         # (the residue distribution) in registers -- the clock the chip holds under that load bounds
         # any int8 GEMM on such data
@@ -552,12 +614,6 @@ def main():
         if ceiling > 0:
             roofline["data_bound_ceiling"] = round(ceiling, 1)
             roofline["frac_of_data_bound_ceiling"] = round(achieved / ceiling, 4)
-        if not sharded and not rows_accurate:
-            extra["phase_ms"] = {"scaling": round(avg[0], 4), "int8_products": round(avg[1], 4),
-                                 "inverse_scaling": round(avg[3], 4)}
-            roofline["composite"] = composite_roofline(work_alg, ms_per_step, extra["phase_ms"])
-        elif sharded:
-            roofline["composite"] = composite_roofline(work_alg, ms_per_step, None, world)
         if not args.no_dgemm and kind == "d" and (world == 1 or sharded):
             # the vendor DGEMM of the same shape on ONE GPU (rocBLAS through torch)
             Ar, Br = A.t(), B.t()
@@ -573,44 +629,16 @@ def main():
             extra["rocblas_dgemm_tflops_1gpu"] = round(dg, 2)
             extra["vs_rocblas_dgemm_1gpu"] = round(value / dg, 3)
         gpu_C = C if (world == 1 and kind == "d" and fast and N == 14) else None
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev, gpu_C)
-        workload, metric = labels(W)
-        out = {
-            "metric": metric,
-            "value": round(value, 3),
-            "unit": "TFLOP/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "strong" if sharded else ("weak" if world > 1 else "single"),
-            "vs_baseline": round(value / world / GH200_PUBLISHED_TFLOPS, 3) if (wl_name == "cfg2" and not custom) else None,
-            "vs_baseline_ref": "GH200 published OS2-fast-14 8192 (72.13 TFLOP/s, BASELINE.md); per-GPU ratio",
-            "dtype": "i8",
-            "io_dtype": {"d": "f64", "dfd": "f64*f32->f64", "z": "c128"}[kind],
-            "data": "synthetic: hiprand XORWOW (U-0.5)*exp(0.5*N(0,1)), seed 123456, A == B as in the reference "
-                    "driver" + (" (row partition: rank r's A seed 123456+r)" if (world > 1 and not sharded) else ""),
-            "config": {"workload": workload, "m": m, "n": n, "k": k, "num_moduli": N, "fastmode": fast,
-                       "parallelism": (("moduli x column blocks" if sharded else "rows") + f" x{world}")
-                       if world > 1 else "single",
-                       "world_size": world, "backend": backend or "none",
-                       "output": ("C gathered on rank 0" if args.gather else "C distributed by column blocks")
-                       if sharded else "C on each rank"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
-        if sharded:
-            out["config"]["unit_order"] = args.order
-            out["config"]["dist_side_stream"] = GD.side_stream_enabled() and backend == "nccl"
-            out["config"]["dist_timeout_s"] = float(os.environ.get("GEMMUL8_DIST_TIMEOUT", "300"))
-        out.update(extra)
-        print(json.dumps(out), flush=True)
+        report["cpu"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev, gpu_C)
+        print(json.dumps(line()), flush=True)
     if world > 1:
         import torch.distributed as dist
-        arm("teardown")
-        dist.barrier()
-        dist.destroy_process_group()
+        arm("teardown", lambda msg: None)  # the line is out (rank 0) or not this rank's to print
+        try:
+            dist.barrier()
+            dist.destroy_process_group()
+        except Exception as e:  # a peer that left after a stuck optional phase: the line stands
+            print(f"bench: teardown: {type(e).__name__}: {str(e)[:200]}", file=sys.stderr, flush=True)
     if wd:
         wd.disarm()
         wd.close()

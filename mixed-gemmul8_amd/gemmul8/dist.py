@@ -100,21 +100,25 @@ class StageWatchdog:
 
     ``arm(phase)`` starts a phase; ``disarm()`` ends it.  The message on stderr names the phase, this rank's
     last recorded step (``progress``: the transfer stage posted last and its peers) and how long ago it was
-    recorded.  The process exits with os._exit from the watchdog thread: no exec, nothing restarted."""
+    recorded.  The process exits with os._exit from the watchdog thread: no exec, nothing restarted.
+    ``arm(phase, on_fire)`` makes the phase optional (work after the measurement): when it outlives the limit,
+    ``on_fire(message)`` runs on the watchdog thread (bench.py: rank 0 prints its line with what it has
+    measured) and the process exits with status 0, so a stuck extra does not void the measurement."""
 
     def __init__(self, limit_s, rank=0, out=None, exit=True):
         self.limit_s, self.rank, self.out = float(limit_s), rank, out or sys.stderr
-        self._phase, self._since = None, 0.0
+        self._phase, self._since, self._on_fire = None, 0.0, None
         self._cv = threading.Condition()
         self._stop = False
         self.fired = None  # the message (tests pass exit=False)
+        self.exit_status = None  # the status the process exits (or, with exit=False, would exit) with
         self.exit = exit
         self._thr = threading.Thread(target=self._run, name="gemmul8-watchdog", daemon=True)
         self._thr.start()
 
-    def arm(self, phase):
+    def arm(self, phase, on_fire=None):
         with self._cv:
-            self._phase, self._since = phase, time.monotonic()
+            self._phase, self._since, self._on_fire = phase, time.monotonic(), on_fire
             self._cv.notify()
 
     def disarm(self):
@@ -145,8 +149,15 @@ class StageWatchdog:
                        f"({time.monotonic() - p['t']:.1f} s ago)")
                 self.fired = msg
                 print(msg, file=self.out, flush=True)
+                self.exit_status = 3
+                if self._on_fire is not None:
+                    self.exit_status = 0
+                    try:
+                        self._on_fire(msg)
+                    except Exception as e:  # the exit below must happen whatever the report does
+                        print(f"gemmul8 watchdog: report failed: {type(e).__name__}: {e}", file=self.out, flush=True)
                 if self.exit:
-                    os._exit(3)
+                    os._exit(self.exit_status)
                 self._phase = None
 
 

@@ -118,3 +118,30 @@ def test_watchdog_reports_the_stage_in_flight():
             assert part in out.getvalue()
     finally:
         wd.close()
+
+
+def test_watchdog_optional_phase_reports_and_exits_zero():
+    """a phase armed with on_fire (bench.py: the work after the timed region) hands the message to the
+    callback (rank 0 prints the line measured so far) and exits with status 0, not 3"""
+    out, got = io.StringIO(), []
+    wd = GD.StageWatchdog(0.2, rank=0, out=out, exit=False)
+    try:
+        wd.arm("variants: moduli_columns_gathered", got.append)
+        deadline = time.time() + 5
+        while wd.fired is None and time.time() < deadline:
+            time.sleep(0.05)
+        assert wd.fired is not None and wd.exit_status == 0
+        assert got == [wd.fired] and "variants: moduli_columns_gathered" in got[0]
+        # a failing callback is reported and does not stop the exit
+        wd.arm("report", lambda msg: 1 / 0)
+        deadline = time.time() + 5
+        while "report failed" not in out.getvalue() and time.time() < deadline:
+            time.sleep(0.05)
+        assert "ZeroDivisionError" in out.getvalue() and wd.exit_status == 0
+        wd.arm("timed steps")  # a measured phase stays fatal
+        deadline = time.time() + 5
+        while wd.exit_status != 3 and time.time() < deadline:
+            time.sleep(0.05)
+        assert wd.exit_status == 3
+    finally:
+        wd.close()
