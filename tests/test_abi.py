@@ -69,6 +69,28 @@ def test_work_size_and_errors_host_only():
     assert lib.gemmul8_gemm(*args(14, k=(1 << 19) - 63, fast=0)) == -4  # accurate: int32 bound product
 
 
+def test_crt_parts_errors_host_only():
+    """gemmul8_crt_partial / gemmul8_crt_finish (the reduce of partial CRT sums) reject bad arguments before
+    anything touches the device, with the codes include/gemmul8_c.h gives; empty outputs are a no-op"""
+    lib = ctypes.CDLL(LIB)
+    p, sz, u, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int
+    lib.gemmul8_crt_partial.restype = i
+    lib.gemmul8_crt_partial.argtypes = [p, sz, sz, sz, u, i, i, p, u, u, p, sz]
+    lib.gemmul8_crt_finish.restype = i
+    lib.gemmul8_crt_finish.argtypes = [p, sz, sz, sz, u, i, i, p, p, p, sz, p, p, sz]
+    part = lambda N=14, tc=0, ct=0, j0=0, j1=14, lds=8, m=8: lib.gemmul8_crt_partial(
+        None, m, 8, 8, N, tc, ct, None, j0, j1, None, lds)
+    fin = lambda N=14, tc=0, ct=0, lds=8, ldc=8, m=8: lib.gemmul8_crt_finish(
+        None, m, 8, 8, N, tc, ct, None, None, None, ldc, None, None, lds)
+    assert part(N=1) == -1 and part(N=21) == -1 and fin(N=1) == -1
+    assert part(ct=1) == fin(ct=1) == -5           # complex: unsupported (real outputs only)
+    assert part(tc=2) == fin(tc=2) == -2           # complex C
+    assert part(lds=7) == fin(lds=7) == -4         # lds < m
+    assert fin(ldc=7) == -4
+    assert part(j0=3, j1=2) == -1 and part(j1=15) == -1  # moduli range
+    assert part(m=0, lds=0) == 0 and fin(m=0, lds=0, ldc=0) == 0
+
+
 def test_complex_karatsuba_layout():
     """complex compute types run Karatsuba sub-products (3 per modulus, csrc/oz2_common.hpp); the
     workspace also holds the accurate-mode big-matrix bound plane; real layouts are unchanged"""
