@@ -241,14 +241,17 @@ def make_operands(kind, m, n, k, seed_a, dev):
     return G.randmat(m, k, torch.float64, 0.5, seed_a, dev), G.randmat(k, n, tb, 0.5, 123456, dev), torch.float64
 
 
-def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lambda name: None):
+def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lambda name: None, out=None):
     """SURVEY.md 8(e)'s partitions side by side, after the timed region, same operands (a few steps each):
     the default (modulus, column block) units with C gathered on the root; whole moduli per rank with the residue
     planes sent to the root and the root's CRT (variant (i)); row blocks of C, all moduli per rank, no exchange
     (variant (ii), strong scaling); its 2-D form (output blocks on a near-square rank grid); and the north star's
     reduce of FP64 partial CRT sums (gemm_moduli_reduce: two m x n double accumulators to the root; C within a
-    few ulp, not bit-identical)."""
+    few ulp, not bit-identical).  Each result goes into `out` as soon as it is measured, so a line printed after a
+    later variant got stuck still carries it."""
     steps, warm = 3, 1
+    out = {} if out is None else out
+    flops = 2.0 * m * n * k
 
     stall = os.environ.get("GEMMUL8_BENCH_REHEARSE_STALL")  # rehearsal of the fail-soft path (DESIGN.md 8)
 
@@ -265,13 +268,14 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lam
                 fn()
             barrier(world)
         except Exception as e:  # a variant must not cost the main line (e.g. a collective the backend lacks)
-            return f"failed: {type(e).__name__}: {str(e)[:200]}"
-        return reduce_max(time.perf_counter() - t0, world) / steps * 1e3
+            out[name] = f"failed: {type(e).__name__}: {str(e)[:200]}"
+            return
+        v = reduce_max(time.perf_counter() - t0, world) / steps * 1e3
+        out[name] = {"ms_per_step": round(v, 3), "tflops": round(flops / (v * 1e-3) / 1e12, 1)}
 
-    out = {}
-    out["moduli_columns_gathered"] = timed("moduli_columns_gathered",
+    timed("moduli_columns_gathered",
         lambda: GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, gather=True, ops=ops))
-    out["moduli_whole_planes_to_root"] = timed("moduli_whole_planes_to_root",
+    timed("moduli_whole_planes_to_root",
         lambda: GD.gemm_moduli_planes_to_root(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, ops=ops))
     r0, r1 = GD.blocks(m, world)[rank]
     if r1 > r0:
@@ -281,7 +285,7 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lam
         rows = lambda: G.gemm(G.OP_N, G.OP_N, r1 - r0, n, k, 1.0, Ar, m, B, k, 0.0, Cr, r1 - r0, N, fast, wr)
     else:
         rows = lambda: None
-    out["row_blocks_all_moduli"] = timed("row_blocks_all_moduli", rows)
+    timed("row_blocks_all_moduli", rows)
     if r1 > r0:
         del wr, Cr
     # 2-D output blocks, all moduli per rank (grid R x Q = W with R, Q closest to sqrt(W)): each rank reads and
@@ -296,17 +300,15 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lam
         blk = lambda: G.gemm(G.OP_N, G.OP_N, a1 - a0, b1 - b0, k, 1.0, Ab, m, Bb, k, 0.0, Cb, a1 - a0, N, fast, wb)
     else:
         blk = lambda: None
-    out[f"output_blocks_{R}x{Q}_all_moduli"] = timed(f"output_blocks_{R}x{Q}_all_moduli", blk)
+    timed(f"output_blocks_{R}x{Q}_all_moduli", blk)
     if fast and a1 > a0 and b1 > b0:
         del wb, Cb
     # the north star's partition as built (gemm_moduli_reduce): whole moduli per rank, partial FP64 CRT sums,
     # one sum-reduce of the two m x n planes to the root, the root's finishing CRT (C within ulps, not bit-identical)
-    out["moduli_partial_sums_reduce"] = timed("moduli_partial_sums_reduce",
+    timed("moduli_partial_sums_reduce",
         lambda: GD.gemm_moduli_reduce(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, ops=ops))
     torch.cuda.empty_cache()
-    flops = 2.0 * m * n * k
-    return {kk: ({"ms_per_step": round(v, 3), "tflops": round(flops / (v * 1e-3) / 1e12, 1)}
-                 if isinstance(v, float) else v) for kk, v in out.items()}
+    return out
 
 
 def select_workload(args, world):
@@ -602,8 +604,9 @@ def main():
 
     if sharded and kind == "d" and not args.no_variants:
         # last of the collective phases: each variant is a phase of its own for the watchdog
-        extra["variants"] = time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops,
-                                          arm=lambda name: arm(f"variants: {name}", soft))
+        extra["variants"] = {}
+        time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops,
+                      arm=lambda name: arm(f"variants: {name}", soft), out=extra["variants"])
 
     if rank == 0:
         arm("report", soft)

@@ -575,6 +575,9 @@ def gemm_moduli_planes_to_root(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14,
     parts = moduli_partition(num_moduli, world)
     j0, j1 = parts[rank]
     st = ops.prepare(opA, opB, m, n, k, A, lda, B, ldb, num_moduli, fastmode, out_dtype, computeType)
+    with _PROGRESS_LOCK:
+        _PROGRESS["call"] += 1
+    progress("planes to root: shifts / encode", f"moduli [{j0}, {j1})")
     if j1 > j0 or rank == root:  # every shift on every such rank (a root without moduli needs them for the CRT)
         ops.stats(st, (0, m), (0, n))
         if not fastmode:
@@ -588,9 +591,11 @@ def gemm_moduli_planes_to_root(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14,
             ops.products(st, j, j + 1, 0, n)
             if host_sync:
                 ops.sync()
+            progress("planes to root: send", f"plane {j} to rank {root}")
             reqs += dist.batch_isend_irecv([dist.P2POp(dist.isend, x, groot, group) for x in ops.chunks(st, j, 0, n)])
         for q in reqs:
             q.wait()
+        progress("done")
         return None
     rcv = [dist.P2POp(dist.irecv, x, _global(group, r), group)
            for r, (a, b) in enumerate(parts) if r != root for j in range(a, b) for x in ops.chunks(st, j, 0, n)]
@@ -605,9 +610,12 @@ def gemm_moduli_planes_to_root(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14,
             reqs = dist.batch_isend_irecv(rcv)
     for j in range(j0, j1):
         ops.products(st, j, j + 1, 0, n)
+    progress("planes to root: receive", f"{num_moduli - (j1 - j0)} planes from {world - 1} ranks")
     for q in reqs:
         q.wait()
-    return ops.recombine(st, 0, n)
+    C = ops.recombine(st, 0, n)
+    progress("done")
+    return C
 
 
 def gemm_moduli_reduce(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None, group=None,
