@@ -1,0 +1,164 @@
+"""GPU: gemmul8.dist's NCCL branch -- stream-ordered transfers, receive-only stages on a side stream, no host
+synchronisation -- run with 2 or 3 ranks as threads on one GPU through tests/fake_nccl.py, a stand-in for
+ProcessGroupNCCL's stream semantics (a one-GPU box cannot run RCCL with more than one rank).  The gloo tests
+cover the host-synchronised branch only.  Every rank runs the real native steps on its own compute stream with its
+own workspace; several calls follow each other through the same workspaces without a host sync, so a missing
+stream dependency (a transfer reading residues before their product launch, a receive overwriting columns the
+previous call's CRT still reads, the CRT starting before the last receive) shows up as wrong bits against the
+single gemmul8_gemm call.
+"""
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from fake_nccl import FakeNcclWorld, run_ranks  # noqa: E402
+from test_gpu_phases import _rand, _same, _single  # noqa: E402
+
+
+DELAY = 200_000  # GPU cycles of spin before every received copy (~0.1 ms): transfers always land late
+
+
+def _world(W, monkeypatch, delay=DELAY):
+    from gemmul8 import dist as GD
+    world = FakeNcclWorld(W, delay_cycles=delay)
+    monkeypatch.setattr(GD, "dist", world.module)
+    return world
+
+
+def _inputs(m, n, k, seeds, dtype):
+    import torch
+    data = [(_rand(m, k, s, dtype), _rand(k, n, s + 1, dtype) * (10.0 ** (s % 3))) for s in seeds]
+    torch.cuda.synchronize()
+    return data
+
+
+def _on_own_stream(fn):
+    """fn() on a fresh compute stream of the calling rank thread; waits for it before returning"""
+    import torch
+    comp = torch.cuda.Stream()
+    with torch.cuda.stream(comp):
+        out = fn()
+    comp.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("W,side", [(2, True), (3, True), (3, False)])
+def test_exchange_stream_ordered_back_to_back(W, side, monkeypatch):
+    """three calls with different operands per rank, back to back on one compute stream: each rank's column block
+    equals the single call's, bit for bit; with and without the side stream for receive-only stages"""
+    import torch
+    from gemmul8 import dist as GD
+    if not side:
+        monkeypatch.setenv("GEMMUL8_DIST_SIDE_STREAM", "0")
+    world = _world(W, monkeypatch)
+    m, n, k, N = 1000, 1536, 1100, 14
+    data = _inputs(m, n, k, (1, 3, 5), torch.float64)
+    refs = [_single(A, B, N, True, torch.float64) for A, B in data]
+    plan = GD.ShardPlan(m, n, N, W)
+
+    def rank(r):
+        ops = GD.HipShardOps()
+        return _on_own_stream(lambda: [GD.matmul_moduli(A, B, N, True, gather=False, ops=ops) for A, B in data])
+
+    res = run_ranks(world, rank)
+    for r in range(W):
+        c0, c1 = plan.cols[r]
+        for i in range(len(data)):
+            assert _same(res[r][i], refs[i][:, c0:c1]), (r, i)
+    assert world.calls["batch_isend_irecv"] >= W * plan.stages // 2 and world.calls["all_gather"] == 3 * W
+
+
+def test_gather_accurate_and_complex(monkeypatch):
+    """C gathered on the root (the blocks received concurrently), accurate mode (the bound maxima MAX-combined
+    on the communication streams), complex Karatsuba operands (three residue sub-planes per transfer)"""
+    import torch
+    import gemmul8 as G
+    from gemmul8 import dist as GD
+    W = 3
+    world = _world(W, monkeypatch)
+    m, n, k, N = 520, 768, 700, 14  # (every rank owns columns: blocks of 256)
+    (A, B), (A2, B2) = _inputs(m, n, k, (7, 9), torch.float64)
+    mc, nc, kc, Nc = 1024, 768, 3072, 12
+    (Ac, Bc), = _inputs(mc, nc, kc, (11,), torch.complex128)
+    assert G.layout(mc, nc, kc, Nc, G.COMPLEX_BIG_MATRIX_ENCODE)["nsub"] == 3
+    ref_f = _single(A, B, N, True, torch.float64)
+    ref_a = _single(A2, B2, N, False, torch.float64)
+    ref_c = _single(Ac, Bc, Nc, True, torch.complex128)
+    plan_c = GD.ShardPlan(mc, nc, Nc, W)
+
+    def rank(r):
+        ops = GD.HipShardOps()
+
+        def calls():
+            return (GD.matmul_moduli(A, B, N, True, gather=True, ops=ops),
+                    GD.matmul_moduli(A2, B2, N, False, gather=True, ops=ops),
+                    GD.matmul_moduli(A2, B2, N, False, gather=False, ops=ops),
+                    GD.matmul_moduli(Ac, Bc, Nc, True, gather=False, ops=ops))
+        return _on_own_stream(calls)
+
+    res = run_ranks(world, rank)
+    assert _same(res[0][0], ref_f) and _same(res[0][1], ref_a)
+    assert all(res[r][0] is None and res[r][1] is None for r in range(1, W))
+    plan = GD.ShardPlan(m, n, N, W)
+    for r in range(W):
+        c0, c1 = plan.cols[r]
+        assert _same(res[r][2], ref_a[:, c0:c1]), r
+        c0, c1 = plan_c.cols[r]
+        assert _same(res[r][3], ref_c[:, c0:c1]), r
+    assert world.calls["all_reduce"] == 2 * W  # the two accurate calls
+
+
+def test_planes_to_root_and_partial_sums_reduce(monkeypatch):
+    """the two comparison partitions bench.py times: whole residue planes sent to the root (bit-identical C) and
+    the north star's sum-reduce of partial CRT sums (C1 exact, C2 reordered: within 2^-40 of max |C|)"""
+    import torch
+    import gemmul8 as G
+    from gemmul8 import dist as GD
+    W = 3
+    world = _world(W, monkeypatch)
+    m, n, k, N = 700, 600, 900, 14
+    data = _inputs(m, n, k, (13, 15), torch.float64)
+    refs = [_single(A, B, N, True, torch.float64) for A, B in data]
+
+    def rank(r):
+        ops = GD.HipShardOps()
+
+        def calls():
+            out = []
+            for A, B in data:
+                out.append(GD.gemm_moduli_planes_to_root(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, ops=ops))
+                out.append(GD.gemm_moduli_reduce(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, ops=ops))
+            return out
+        return _on_own_stream(calls)
+
+    res = run_ranks(world, rank)
+    for i, ref in enumerate(refs):
+        planes, red = res[0][2 * i], res[0][2 * i + 1]
+        assert _same(planes.t(), ref)
+        err = (red.t() - ref).abs().max().item()
+        assert err <= 2.0 ** -40 * ref.abs().max().item(), (i, err)
+    assert all(x is None for r in range(1, W) for x in res[r])
+    assert world.calls["reduce"] == 2 * W
+
+
+def test_negative_control_consumer_without_wait(monkeypatch):
+    """the harness catches a missing dependency: with Work.wait() made a no-op, the CRT no longer waits for the
+    received residue columns (which land late), and the blocks differ from the single call"""
+    import torch
+    import fake_nccl
+    from gemmul8 import dist as GD
+    W = 2
+    world = _world(W, monkeypatch, delay=2_000_000)
+    monkeypatch.setattr(fake_nccl._Work, "wait", lambda self: True)
+    m, n, k, N = 1000, 1536, 1100, 14
+    (A, B), = _inputs(m, n, k, (1,), torch.float64)
+    ref = _single(A, B, N, True, torch.float64)
+    plan = GD.ShardPlan(m, n, N, W)
+    res = run_ranks(world, lambda r: _on_own_stream(
+        lambda: GD.matmul_moduli(A, B, N, True, gather=False, ops=GD.HipShardOps())))
+    bad = [r for r in range(W) if not _same(res[r], ref[:, plan.cols[r][0]:plan.cols[r][1]])]
+    assert bad, "the sabotaged run still matched: the harness would not see a missing wait"
