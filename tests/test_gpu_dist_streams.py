@@ -154,11 +154,30 @@ def test_negative_control_consumer_without_wait(monkeypatch):
     W = 2
     world = _world(W, monkeypatch, delay=2_000_000)
     monkeypatch.setattr(fake_nccl._Work, "wait", lambda self: True)
+    # operands no other test uses: a recycled workspace of an earlier test cannot already hold these residues
     m, n, k, N = 1000, 1536, 1100, 14
-    (A, B), = _inputs(m, n, k, (1,), torch.float64)
+    (A, B), = _inputs(m, n, k, (31,), torch.float64)
     ref = _single(A, B, N, True, torch.float64)
     plan = GD.ShardPlan(m, n, N, W)
     res = run_ranks(world, lambda r: _on_own_stream(
         lambda: GD.matmul_moduli(A, B, N, True, gather=False, ops=GD.HipShardOps())))
     bad = [r for r in range(W) if not _same(res[r], ref[:, plan.cols[r][0]:plan.cols[r][1]])]
     assert bad, "the sabotaged run still matched: the harness would not see a missing wait"
+
+
+def test_row_blocks_accurate_gathered(monkeypatch):
+    """matmul_rows under the NCCL branch: accurate mode MAX-combines the bound product's column maxima, the root
+    gathers the row blocks; equal to the single call over all rows, bit for bit"""
+    import torch
+    from gemmul8 import dist as GD
+    W = 3
+    world = _world(W, monkeypatch)
+    m, n, k, N = 900, 500, 800, 12
+    (A, B), = _inputs(m, n, k, (21,), torch.float64)
+    ref = _single(A, B, N, False, torch.float64)
+    bl = GD.blocks(m, W)
+    res = run_ranks(world, lambda r: _on_own_stream(
+        lambda: GD.matmul_rows(A[bl[r][0]:bl[r][1]].contiguous(), B, N, False, gather=True, ops=GD.HipOps())))
+    assert _same(res[0], ref)
+    assert res[1] is None and res[2] is None
+    assert world.calls["all_reduce"] == W
