@@ -43,8 +43,9 @@ def _single(A, B, N, fast, out_dtype):
 
 def _same(a, b):
     import torch
-    # (reshape(-1): a one-column block of a column-major buffer counts as contiguous with a stride of m)
-    return a.shape == b.shape and torch.equal(a.reshape(-1).view(torch.uint8), b.reshape(-1).view(torch.uint8))
+    # (flattened first: a one-column block of a column-major buffer counts as contiguous with a stride of m)
+    flat = lambda x: x.reshape(-1).contiguous().view(torch.uint8)
+    return a.shape == b.shape and torch.equal(flat(a), flat(b))
 
 
 @pytest.mark.parametrize("m,n,k,N,fast,dt", [
