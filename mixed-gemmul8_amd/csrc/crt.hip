@@ -66,27 +66,82 @@ __device__ __forceinline__ double crt_value_const(const uint8_t (&r)[N], std::in
     }
 }
 
+// The same values for the CRT_ROWS rows of a lane at once, moduli outermost: each weight pair is used for the
+// lane's rows right after it is materialised, so only one pair is live (per row the fma chains run i ascending,
+// as in crt_value_const: the same bits).  With the rows innermost the compiler kept all 2N weights live across
+// the row loop and parked most of them in VGPR lanes.
+// An f64 constant materialised in an SGPR pair where it is used: the two moves are volatile, so they are
+// not hoisted out of the column loop (hoisted, the 2N weights overflow the SGPRs and are spilled to VGPR lanes)
+template <uint64_t BITS> __device__ __forceinline__ double sconst() {
+    uint32_t lo, hi;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(lo) : "i"((uint32_t)BITS));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(hi) : "i"((uint32_t)(BITS >> 32)));
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+template <unsigned N, bool NUMM1, int R, typename W, unsigned... I>
+__device__ __forceinline__ void crt_rows_const(const W (&w)[N], double (&out)[R], std::integer_sequence<unsigned, I...>) {
+    constexpr double invM = oz2_invM[N - 2], M1 = oz2_M_hi[N - 2], M2 = oz2_M_lo[N - 2];
+    double C1[R] = {}, C2[R] = {};
+    auto step = [&](auto ic) {
+        constexpr unsigned i = decltype(ic)::value;
+        const W x = w[i];
+        const double hi = sconst<__builtin_bit_cast(uint64_t, w_hi<N, NUMM1, i>())>();
+        const double lo = NUMM1 ? 0.0 : sconst<__builtin_bit_cast(uint64_t, w_lo<N, i>())>();
+#pragma unroll
+        for (int e = 0; e < R; ++e) {
+            const double r = (double)(uint8_t)(x >> (8 * e));
+            C1[e] = __builtin_fma(hi, r, C1[e]);
+            if constexpr (!NUMM1) C2[e] = __builtin_fma(lo, r, C2[e]);
+        }
+    };
+    (step(std::integral_constant<unsigned, I>{}), ...);
+#pragma unroll
+    for (int e = 0; e < R; ++e) {
+        if constexpr (NUMM1) {
+            const double quot = -__builtin_rint(C1[e] * invM);
+            out[e] = __builtin_fma(quot, M1, C1[e]);
+        } else {
+            const double quot = -__builtin_rint(__builtin_fma(C1[e], invM, C2[e] * invM));
+            const double t1 = __builtin_fma(quot, M1, C1[e]) + C2[e];
+            out[e] = __builtin_fma(quot, M2, t1);
+        }
+    }
+}
+#ifndef OZ2_CRT_MODOUTER
+#define OZ2_CRT_MODOUTER 1  // A/B builds: 0 = the per-row chains (crt_value_const) in the Karatsuba CRT
+#endif
+#ifndef OZ2_CRT_MODOUTER_ALL
+#define OZ2_CRT_MODOUTER_ALL 0  // A/B builds: 1 = the same order in the real and big-matrix complex CRT (the
+                                // real CRT is bound by HBM: same time; N = 10 then needs 135 VGPRs)
+#endif
+#ifndef OZ2_KARA_ROWS
+#define OZ2_KARA_ROWS 8  // rows per lane of the Karatsuba CRT (A/B builds: 4 -- 127 VGPRs and 4 waves per SIMD
+                         // instead of 155 and 3, the same time: profiles/r04/j/lib_ab.txt)
+#endif
+// residue word of R consecutive rows of one plane (one byte per row)
+template <int R> using RowWord = std::conditional_t<R == 8, uint64_t, uint32_t>;
+
 #ifndef OZ2_CRT_NT
 #define OZ2_CRT_NT 0  // probe builds: 1 = non-temporal residue loads, 2 = non-temporal C stores, 3 = both
 #endif
 // residues of rows [off, off+8) of every plane; the fast path is one 8-byte load per plane
-template <unsigned N>
-__device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fast, int nr, uint64_t (&w)[N]) {
+template <unsigned N, typename W = uint64_t>
+__device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fast, int nr, W (&w)[N]) {
     if (fast) {
         // one per-lane pointer stepped plane by plane (N scalar plane bases would spill the SGPRs)
         const uint8_t *q = a.R + off;
 #pragma unroll
         for (unsigned i = 0; i < N; ++i) {
-            if (OZ2_CRT_NT & 1) w[i] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t *>(q));
-            else w[i] = *reinterpret_cast<const uint64_t *>(q);
+            if (OZ2_CRT_NT & 1) w[i] = __builtin_nontemporal_load(reinterpret_cast<const W *>(q));
+            else w[i] = *reinterpret_cast<const W *>(q);
             q += a.planeR;
             asm volatile("" : "+v"(q));
         }
     } else {
 #pragma unroll
         for (unsigned i = 0; i < N; ++i) {
-            uint64_t x = 0;
-            for (int e = 0; e < nr; ++e) x |= (uint64_t)a.R[i * a.planeR + off + e] << (8 * e);
+            W x = 0;
+            for (int e = 0; e < nr; ++e) x |= (W)a.R[i * a.planeR + off + e] << (8 * e);
             w[i] = x;
         }
     }
@@ -244,28 +299,37 @@ template <int P> __device__ __forceinline__ uint32_t kara_sub_dword(uint32_t x3,
     constexpr uint32_t LO = 0x00ff00ffu;
     return lanes(x3 & LO, sum & LO) | (lanes((x3 >> 8) & LO, (sum >> 8) & LO) << 8);
 }
-template <unsigned N, unsigned... I>
-__device__ __forceinline__ void kara_pair_words(const uint64_t (&w1)[N], const uint64_t (&w2)[N], uint64_t (&re)[N],
-                                                uint64_t (&sum)[N], std::integer_sequence<unsigned, I...>) {
+template <unsigned N, typename W, unsigned... I>
+__device__ __forceinline__ void kara_pair_words(const W (&w1)[N], const W (&w2)[N], W (&re)[N], W (&sum)[N],
+                                                std::integer_sequence<unsigned, I...>) {
     auto one = [&](auto ic) {
         constexpr unsigned i = decltype(ic)::value;
-        uint32_t r0, s0, r1, s1;
+        uint32_t r0, s0;
         kara_pair_dword<oz2_p[i]>((uint32_t)w1[i], (uint32_t)w2[i], r0, s0);
-        kara_pair_dword<oz2_p[i]>((uint32_t)(w1[i] >> 32), (uint32_t)(w2[i] >> 32), r1, s1);
-        re[i] = (uint64_t)r0 | ((uint64_t)r1 << 32);
-        sum[i] = (uint64_t)s0 | ((uint64_t)s1 << 32);
+        if constexpr (sizeof(W) == 8) {
+            uint32_t r1, s1;
+            kara_pair_dword<oz2_p[i]>((uint32_t)(w1[i] >> 32), (uint32_t)(w2[i] >> 32), r1, s1);
+            re[i] = (uint64_t)r0 | ((uint64_t)r1 << 32);
+            sum[i] = (uint64_t)s0 | ((uint64_t)s1 << 32);
+        } else {
+            re[i] = r0;
+            sum[i] = s0;
+        }
         asm volatile("" : "+v"(re[i]), "+v"(sum[i]));  // computed here, so P1's and P2's words die here
     };
     (one(std::integral_constant<unsigned, I>{}), ...);
 }
-template <unsigned N, unsigned... I>
-__device__ __forceinline__ void kara_sub_words(const uint64_t (&w3)[N], uint64_t (&sum_im)[N],
-                                               std::integer_sequence<unsigned, I...>) {
+template <unsigned N, typename W, unsigned... I>
+__device__ __forceinline__ void kara_sub_words(const W (&w3)[N], W (&sum_im)[N], std::integer_sequence<unsigned, I...>) {
     auto one = [&](auto ic) {
         constexpr unsigned i = decltype(ic)::value;
         const uint32_t lo = kara_sub_dword<oz2_p[i]>((uint32_t)w3[i], (uint32_t)sum_im[i]);
-        const uint32_t hi = kara_sub_dword<oz2_p[i]>((uint32_t)(w3[i] >> 32), (uint32_t)(sum_im[i] >> 32));
-        sum_im[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        if constexpr (sizeof(W) == 8) {
+            const uint32_t hi = kara_sub_dword<oz2_p[i]>((uint32_t)(w3[i] >> 32), (uint32_t)(sum_im[i] >> 32));
+            sum_im[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+        } else {
+            sum_im[i] = lo;
+        }
         asm volatile("" : "+v"(sum_im[i]));
     };
     (one(std::integral_constant<unsigned, I>{}), ...);
@@ -294,90 +358,129 @@ __device__ __forceinline__ void kara_words(const uint64_t (&w1)[N], const uint64
 // EPV (so the EPV consecutive rows of one 16-byte read stay adjacent and in order) that differs between
 // the lanes whose 8-row groups share a 256-byte LDS row; unswizzled, the 8-byte (f64) writes of a wave
 // hit the same banks 16 ways (complex f64: 32 ways), swizzled 4 ways
-template <typename E> __device__ __forceinline__ int crt_slot(int l, int e) {
+template <typename E, int R = CRT_ROWS> __device__ __forceinline__ int crt_slot(int l, int e) {
     constexpr int EPV = 16 / sizeof(E);
-    constexpr int SH = sizeof(E) == 4 ? 3 : sizeof(E) == 8 ? 2 : 1;  // log2 of the lanes per 256-byte row
-    return l * CRT_ROWS + (e ^ ((EPV * (l >> SH)) & (CRT_ROWS - 1)));
+    constexpr int LPR = 256 / (R * (int)sizeof(E));  // lanes per 256-byte row
+    constexpr int SH = LPR >= 8 ? 3 : LPR >= 4 ? 2 : LPR >= 2 ? 1 : 0;
+    return l * R + (e ^ ((EPV * (l >> SH)) & (R - 1)));
 }
 
-template <int OT, bool NUMM1, unsigned N, bool KARA = false>
+template <int OT, bool NUMM1, unsigned N, bool KARA = false, int R = CRT_ROWS>
 __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
+    static_assert(R == CRT_ROWS || KARA, "rows per lane other than CRT_ROWS: Karatsuba form only");
+    using W = RowWord<R>;
     using E = typename OutElem<OT>::T;
     constexpr int EPV = 16 / sizeof(E);  // elements per 16-byte vector
-    __shared__ E buf[4][64 * CRT_ROWS];
+    __shared__ E buf[4][64 * R];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const size_t wrow0 = ((size_t)blockIdx.x * 256 + wv * 64) * CRT_ROWS;
+    const size_t wrow0 = ((size_t)blockIdx.x * 256 + wv * 64) * R;
     if (wrow0 >= a.m) return;  // whole wave beyond the last row (no block-level sync below)
-    const size_t r0 = wrow0 + (size_t)lane * CRT_ROWS;
-    const int nr = r0 >= a.m ? 0 : (a.m - r0 >= CRT_ROWS ? CRT_ROWS : (int)(a.m - r0));
+    const size_t r0 = wrow0 + (size_t)lane * R;
+    const int nr = r0 >= a.m ? 0 : (a.m - r0 >= R ? R : (int)(a.m - r0));
     const bool plain_ab = a.ar == 1.0 && a.ai == 0.0 && a.br == 0.0 && a.bi == 0.0;
     // C is not read at beta = 0 (BLAS), except by the reference's _ab kernels (reference-epilogue mode)
     const bool zero_beta = a.br == 0.0 && a.bi == 0.0 && !(a.ref_epi && !(a.ar == 1.0 && a.ai == 0.0));
-    int16_t sa[CRT_ROWS];
+    int16_t sa[R];
 #pragma unroll
-    for (int e = 0; e < CRT_ROWS; ++e) sa[e] = e < nr ? a.sftA[r0 + e] : 0;
+    for (int e = 0; e < R; ++e) sa[e] = e < nr ? a.sftA[r0 + e] : 0;
     E *wb = buf[wv];
     for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
         const int sB = a.sftB[col];
         if (nr > 0) {
-            uint64_t w[N], wi[N];
+            W w[N], wi[N];
             const size_t off = col * a.ldr + r0;
             if constexpr (KARA) {
                 // real parts from P1, P2 first, then the imaginary parts with P3: two sub-planes' words
                 // live at a time instead of three (occupancy; the residues are the same bytes)
-                uint64_t w1[N], w2[N];
-                load_rows<N>(a, off, nr == CRT_ROWS, nr, w1);
-                load_rows<N>(a, off + a.sub, nr == CRT_ROWS, nr, w2);
+                W w1[N], w2[N];
+                load_rows<N>(a, off, nr == R, nr, w1);
+                load_rows<N>(a, off + a.sub, nr == R, nr, w2);
                 kara_pair_words<N>(w1, w2, w, wi, std::make_integer_sequence<unsigned, N>{});
                 // P3's loads go out after that (an opaque dependency on the last combined word keeps the
                 // compiler from merging them with P1's and P2's), in flight under the real parts
                 size_t off3 = off + 2 * a.sub;
                 asm volatile("" : "+v"(off3) : "v"(wi[N - 1]));
-                uint64_t w3[N];
-                load_rows<N>(a, off3, nr == CRT_ROWS, nr, w3);
+                W w3[N];
+                load_rows<N>(a, off3, nr == R, nr, w3);
+                if constexpr (OZ2_CRT_MODOUTER) {
+                    double v[R];
+                    crt_rows_const<N, NUMM1, R>(w, v, std::make_integer_sequence<unsigned, N>{});
 #pragma unroll
-                for (int e = 0; e < CRT_ROWS; ++e) {
-                    uint8_t r[N];
+                    for (int e = 0; e < R; ++e) {
+                        const double vr = scalbn(v[e], (int)sa[e] + sB);
+                        if constexpr (OT == 2) wb[crt_slot<E, R>(lane, e)].x = vr;
+                        else wb[crt_slot<E, R>(lane, e)].x = __double2float_rn(vr);
+                    }
+                } else {
 #pragma unroll
-                    for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
-                    const double vr = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}),
-                                             (int)sa[e] + sB);
-                    if constexpr (OT == 2) wb[crt_slot<E>(lane, e)].x = vr;
-                    else wb[crt_slot<E>(lane, e)].x = __double2float_rn(vr);
+                    for (int e = 0; e < R; ++e) {
+                        uint8_t r[N];
+#pragma unroll
+                        for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
+                        const double vr = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}),
+                                                 (int)sa[e] + sB);
+                        if constexpr (OT == 2) wb[crt_slot<E, R>(lane, e)].x = vr;
+                        else wb[crt_slot<E, R>(lane, e)].x = __double2float_rn(vr);
+                    }
                 }
                 asm volatile("" ::: "memory");  // the real parts go to LDS now (no merging with the imaginary ones)
                 kara_sub_words<N>(w3, wi, std::make_integer_sequence<unsigned, N>{});
+                if constexpr (OZ2_CRT_MODOUTER) {
+                    double v[R];
+                    crt_rows_const<N, NUMM1, R>(wi, v, std::make_integer_sequence<unsigned, N>{});
 #pragma unroll
-                for (int e = 0; e < CRT_ROWS; ++e) {
-                    uint8_t r[N];
+                    for (int e = 0; e < R; ++e) {
+                        const double vi = scalbn(v[e], (int)sa[e] + sB);
+                        if constexpr (OT == 2) wb[crt_slot<E, R>(lane, e)].y = vi;
+                        else wb[crt_slot<E, R>(lane, e)].y = __double2float_rn(vi);
+                    }
+                } else {
 #pragma unroll
-                    for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(wi[i] >> (8 * e));
-                    const double vi = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}),
-                                             (int)sa[e] + sB);
-                    if constexpr (OT == 2) wb[crt_slot<E>(lane, e)].y = vi;
-                    else wb[crt_slot<E>(lane, e)].y = __double2float_rn(vi);
+                    for (int e = 0; e < R; ++e) {
+                        uint8_t r[N];
+#pragma unroll
+                        for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(wi[i] >> (8 * e));
+                        const double vi = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}),
+                                                 (int)sa[e] + sB);
+                        if constexpr (OT == 2) wb[crt_slot<E, R>(lane, e)].y = vi;
+                        else wb[crt_slot<E, R>(lane, e)].y = __double2float_rn(vi);
+                    }
                 }
             } else {
-                load_rows<N>(a, off, nr == CRT_ROWS, nr, w);
-                if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == CRT_ROWS && (a.imag_off & 7) == 0, nr, wi);
+                load_rows<N>(a, off, nr == R, nr, w);
+                if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == R && (a.imag_off & 7) == 0, nr, wi);
+            }
+            if constexpr (!KARA && OZ2_CRT_MODOUTER_ALL) {
+                double vr[R], vi[R];
+                crt_rows_const<N, NUMM1, R>(w, vr, std::make_integer_sequence<unsigned, N>{});
+                if constexpr (OT >= 2) crt_rows_const<N, NUMM1, R>(wi, vi, std::make_integer_sequence<unsigned, N>{});
+#pragma unroll
+                for (int e = 0; e < R; ++e) {
+                    const int sft = (int)sa[e] + sB;
+                    const double x = scalbn(vr[e], sft);
+                    if constexpr (OT == 0) wb[crt_slot<E, R>(lane, e)] = x;
+                    else if constexpr (OT == 1) wb[crt_slot<E, R>(lane, e)] = __double2float_rn(x);
+                    else if constexpr (OT == 2) wb[crt_slot<E, R>(lane, e)] = make_double2(x, scalbn(vi[e], sft));
+                    else wb[crt_slot<E, R>(lane, e)] = make_float2(__double2float_rn(x), __double2float_rn(scalbn(vi[e], sft)));
+                }
             }
 #pragma unroll
-            for (int e = 0; e < (KARA ? 0 : CRT_ROWS); ++e) {
+            for (int e = 0; e < (KARA || OZ2_CRT_MODOUTER_ALL ? 0 : R); ++e) {
                 uint8_t r[N];
 #pragma unroll
                 for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
                 const int sft = (int)sa[e] + sB;
                 const double vr = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}), sft);
                 if constexpr (OT == 0) {
-                    wb[crt_slot<E>(lane, e)] = vr;
+                    wb[crt_slot<E, R>(lane, e)] = vr;
                 } else if constexpr (OT == 1) {
-                    wb[crt_slot<E>(lane, e)] = __double2float_rn(vr);
+                    wb[crt_slot<E, R>(lane, e)] = __double2float_rn(vr);
                 } else {
 #pragma unroll
                     for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(wi[i] >> (8 * e));
                     const double vi = scalbn(crt_value_const<N, NUMM1>(r, std::make_integer_sequence<unsigned, N>{}), sft);
-                    if constexpr (OT == 2) wb[crt_slot<E>(lane, e)] = make_double2(vr, vi);
-                    else wb[crt_slot<E>(lane, e)] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
+                    if constexpr (OT == 2) wb[crt_slot<E, R>(lane, e)] = make_double2(vr, vi);
+                    else wb[crt_slot<E, R>(lane, e)] = make_float2(__double2float_rn(vr), __double2float_rn(vi));
                 }
             }
         }
@@ -385,10 +488,10 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
         E *Cc = static_cast<E *>(a.C) + col * a.ldc + wrow0;
         const bool vec_ok = (reinterpret_cast<uintptr_t>(Cc) & 15) == 0;
 #pragma unroll
-        for (int j = 0; j < CRT_ROWS / EPV; ++j) {
+        for (int j = 0; j < R / EPV; ++j) {
             const int idx = j * 64 * EPV + lane * EPV;
             E v[EPV];
-            *reinterpret_cast<int4 *>(v) = *reinterpret_cast<const int4 *>(wb + crt_slot<E>(idx / CRT_ROWS, idx % CRT_ROWS));
+            *reinterpret_cast<int4 *>(v) = *reinterpret_cast<const int4 *>(wb + crt_slot<E, R>(idx / R, idx % R));
             if (vec_ok && wrow0 + idx + EPV <= a.m) {
                 if (!plain_ab) {
                     E c[EPV];
@@ -424,7 +527,9 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
 
 template <int OT, bool NUMM1, unsigned N, bool KARA>
 static void launch_crt_n(const CrtArgs &a, dim3 grid, hipStream_t st) {
-    launch(crt_kernel<OT, NUMM1, N, KARA>, grid, dim3(256), st, a);
+    constexpr int R = KARA ? OZ2_KARA_ROWS : CRT_ROWS;
+    grid.x = (unsigned)((a.m + 256 * R - 1) / (256 * R));
+    launch(crt_kernel<OT, NUMM1, N, KARA, R>, grid, dim3(256), st, a);
 }
 
 template <int OT, bool NUMM1, bool KARA = false>

@@ -19,9 +19,9 @@ pytestmark = pytest.mark.skipif(not shutil.which("llvm-readelf", path="/opt/rocm
 FLOORS = {
     "oz2::gemm_i8_persistent_kernel<false, 1, 0>": 2,  # cfg2/3/4 products: 512 threads, 160 KiB LDS, 1 block per CU
     "oz2::gemm_i8_persistent_kernel<true, 1, 0>": 2,   # cfg5 (Karatsuba sub-products)
-    "oz2::crt_kernel<0, false, 14u, false>": 5,        # cfg2/3 CRT
-    "oz2::crt_kernel<0, false, 10u, false>": 5,        # cfg4 CRT
-    "oz2::crt_kernel<2, false, 12u, true>": 3,         # cfg5 CRT (Karatsuba residues)
+    "oz2::crt_kernel<0, false, 14u, false, 8>": 5,     # cfg2/3 CRT
+    "oz2::crt_kernel<0, false, 10u, false, 8>": 5,     # cfg4 CRT
+    "oz2::crt_kernel<2, false, 12u, true, 8>": 3,      # cfg5 CRT (Karatsuba residues)
     "oz2::stats_pair_kernel<16, true>": 8,             # cfg2 shifts
     "oz2::encode_pair_kernel<double, false, false, true, true>": 4,  # cfg2 slices
     "oz2::encode_kernel<double, true, false, false, 0, true>": 2,    # cfg5 slices
