@@ -19,7 +19,10 @@ streams, and the GPU tests run the real native steps through it (tests/test_gpu_
 - synchronous collectives make the caller's current stream wait for their end; a Work's wait() does the same
   for its batch (Work.wait() under ProcessGroupNCCL);
 - delay_cycles > 0 puts a bounded GPU spin (torch.cuda._sleep) in front of every received copy, so transfers
-  land late and a consumer that does not wait for them reads stale columns every time, not by chance.
+  land late.  A consumer that does not wait for them then reads stale columns whenever its stream runs on a
+  hardware queue of its own; HIP maps a process's streams onto GPU_MAX_HW_QUEUES (4 here) queues, and two streams
+  on one queue run in order, so a missing dependency is caught with high probability, not with certainty;
+- drop_receives=True completes receives without copying (the negative control: results must then differ).
 The host side blocks only to match peers (a send's receiver must have posted before the sender's batch returns,
 a receive's sender before the copy is enqueued), which can only deadlock where the stream-ordered NCCL schedule
 would.  Every tensor a communication stream touches is recorded on it for the caching allocator.
@@ -44,10 +47,11 @@ class _Work:
 
 
 class FakeNcclWorld:
-    def __init__(self, world, timeout_s=120.0, delay_cycles=0):
+    def __init__(self, world, timeout_s=120.0, delay_cycles=0, drop_receives=False):
         self.world = world
         self.timeout_s = timeout_s
         self.delay_cycles = int(delay_cycles)
+        self.drop_receives = drop_receives
         self._cv = threading.Condition()
         self._chan = collections.defaultdict(list)       # (src, dst) -> posted sends, in order
         self._recv_next = collections.defaultdict(int)   # (src, dst) -> index of the next receive
@@ -135,7 +139,8 @@ class FakeNcclWorld:
             with torch.cuda.stream(comm):
                 if self.delay_cycles:
                     torch.cuda._sleep(self.delay_cycles)
-                dst.copy_(src)
+                if not self.drop_receives:
+                    dst.copy_(src)
             done = self._event(comm)
             with self._cv:
                 e["done"] = done
