@@ -181,3 +181,11 @@ def test_row_blocks_accurate_gathered(monkeypatch):
     assert _same(res[0], ref)
     assert res[1] is None and res[2] is None
     assert world.calls["all_reduce"] == W
+
+
+
+def test_random_cases():
+    """40 random cases of the NCCL branch (tests/dist_soak.py; tools/probes/fake_nccl_soak.py runs hundreds)"""
+    from dist_soak import soak
+    n, fails = soak(40, 2024)
+    assert n == 0, fails[:3]
