@@ -114,6 +114,10 @@ __device__ __forceinline__ void crt_rows_const(const W (&w)[N], double (&out)[R]
 #define OZ2_CRT_MODOUTER_ALL 0  // A/B builds: 1 = the same order in the real and big-matrix complex CRT (the
                                 // real CRT is bound by HBM: same time; N = 10 then needs 135 VGPRs)
 #endif
+#ifndef OZ2_CRT_MODOUTER_MIN_N
+#define OZ2_CRT_MODOUTER_MIN_N 15  // ... and from this N on regardless: with the rows innermost the real CRT parks
+                                   // 244-820 weight words in VGPR lanes at N = 16-20 (90 at N = 14)
+#endif
 #ifndef OZ2_KARA_ROWS
 #define OZ2_KARA_ROWS 8  // rows per lane of the Karatsuba CRT (A/B builds: 4 -- 127 VGPRs and 4 waves per SIMD
                          // instead of 155 and 3, the same time: profiles/r04/j/lib_ab.txt)
@@ -450,7 +454,8 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
                 load_rows<N>(a, off, nr == R, nr, w);
                 if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == R && (a.imag_off & 7) == 0, nr, wi);
             }
-            if constexpr (!KARA && OZ2_CRT_MODOUTER_ALL) {
+            constexpr bool MO = OZ2_CRT_MODOUTER_ALL || N >= OZ2_CRT_MODOUTER_MIN_N;
+            if constexpr (!KARA && MO) {
                 double vr[R], vi[R];
                 crt_rows_const<N, NUMM1, R>(w, vr, std::make_integer_sequence<unsigned, N>{});
                 if constexpr (OT >= 2) crt_rows_const<N, NUMM1, R>(wi, vi, std::make_integer_sequence<unsigned, N>{});
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
                 }
             }
 #pragma unroll
-            for (int e = 0; e < (KARA || OZ2_CRT_MODOUTER_ALL ? 0 : R); ++e) {
+            for (int e = 0; e < (KARA || MO ? 0 : R); ++e) {
                 uint8_t r[N];
 #pragma unroll
                 for (unsigned i = 0; i < N; ++i) r[i] = (uint8_t)(w[i] >> (8 * e));
