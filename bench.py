@@ -27,6 +27,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import torch
@@ -70,9 +71,22 @@ def parse(argv=None):
     ap.add_argument("--no-dgemm", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="sharded runs: skip timing the other partitions")
     ap.add_argument("--cpu-sample", type=int, default=0, help="CPU baseline size (default: auto)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline OpenMP threads (default: OMP_NUM_THREADS, the host's CPU share for this job)")
     ap.add_argument("--no-single-gpu", action="store_true",
                     help="sharded runs: skip timing the same call on one GPU after the timed region")
     return ap.parse_args(argv)
+
+
+# The line's dicts (extra, its variants, roofline) change after the timed region while the watchdog thread
+# may serialise them (an optional phase got stuck): every such change and every serialisation takes this lock,
+# and nothing that can block runs under it.
+STATE_LOCK = threading.Lock()
+
+
+def put(d, key, value):
+    with STATE_LOCK:
+        d[key] = value
 
 
 def _free_port():
@@ -164,7 +178,7 @@ def _cpu_model():
     return "unknown CPU"
 
 
-def cpu_baseline(size_hint, dev, gpu_C=None):
+def cpu_baseline(size_hint, dev, gpu_C=None, threads_req=0):
     """The oracle (CPU restatement, OpenMP) timed on a bounded sample of the cfg2 workload (same generator,
     fast mode, N = 14) and cfg1 (SGEMM emulation 1024^3, N = 4, fast) in full, both on this host.
     gpu_C: the GPU line's C of the same call (column-major, (n, m) tensor): the oracle's C is compared with it
@@ -173,6 +187,11 @@ def cpu_baseline(size_hint, dev, gpu_C=None):
     import gemmul8 as G
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
+    # threads: every CPU this job is allotted.  On the GPU pool a one-GPU job's share is 16 CPUs of the host
+    # (the harness exports OMP_NUM_THREADS=16 and bounds worker pools to that share) although the affinity mask
+    # lists all of the host's CPUs; --cpu-threads overrides it on a dedicated host
+    if threads_req > 0:
+        O.set_num_threads(threads_req)
     threads = O.num_threads()
     # the full cfg2 size (full size when it fits the time budget): the oracle's int8 products run
     # blocked on AVX-512 VNNI where the host has it (about 4 s at 4096 on 8 threads of this container)
@@ -188,7 +207,11 @@ def cpu_baseline(size_hint, dev, gpu_C=None):
                      f"restatement (int8 products on AVX-512 VNNI: {O.vnni()}) with {threads} OpenMP threads on "
                      f"{_cpu_model()} ({affinity} CPUs in this process's affinity mask, "
                      f"{os.cpu_count()} logical CPUs in the machine)",
-           "threads": threads, "affinity_cpus": affinity, "logical_cpus_machine": os.cpu_count()}
+           "threads": threads, "affinity_cpus": affinity, "logical_cpus_machine": os.cpu_count(),
+           "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+           "threads_policy": ("--cpu-threads" if threads_req > 0 else
+                              "OpenMP default = OMP_NUM_THREADS (the CPUs allotted to a one-GPU job on the GPU pool; "
+                              "the affinity mask shows the whole host, which other jobs share)")}
     dA = torch.from_numpy(np.ascontiguousarray(A.T)).to(dev)
     C1, C2 = G.dd_gemm(dA, dA, n, n, n)
     dC = torch.from_numpy(np.ascontiguousarray(C.T)).to(dev)
@@ -268,10 +291,10 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lam
                 fn()
             barrier(world)
         except Exception as e:  # a variant must not cost the main line (e.g. a collective the backend lacks)
-            out[name] = f"failed: {type(e).__name__}: {str(e)[:200]}"
+            put(out, name, f"failed: {type(e).__name__}: {str(e)[:200]}")
             return
         v = reduce_max(time.perf_counter() - t0, world) / steps * 1e3
-        out[name] = {"ms_per_step": round(v, 3), "tflops": round(flops / (v * 1e-3) / 1e12, 1)}
+        put(out, name, {"ms_per_step": round(v, 3), "tflops": round(flops / (v * 1e-3) / 1e12, 1)})
 
     timed("moduli_columns_gathered",
         lambda: GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, gather=True, ops=ops))
@@ -546,7 +569,9 @@ def main():
     # whose peer failed, say), rank 0 prints the line measured so far and every rank exits with status 0
     if rank == 0:
         def soft(msg):
-            print(json.dumps(line(msg)), flush=True)
+            with STATE_LOCK:
+                text = json.dumps(line(msg))
+            print(text, flush=True)
     else:
         def soft(msg):
             pass
@@ -568,13 +593,13 @@ def main():
             else:
                 emax, emed = 0.0, 0.0
             emax = reduce_max(emax, world)
-            extra["relerr_max"] = emax
-            extra["relerr_median_rank0_columns"] = emed
+            put(extra, "relerr_max", emax)
+            put(extra, "relerr_median_rank0_columns", emed)
         elif world == 1 or rank == 0:
             C1, C2 = G.dd_gemm(A, B, m, n, k)
             emax, emed = G.relerr_dd(Cout, C1, C2)
-            extra["relerr_max"] = emax
-            extra["relerr_median"] = emed
+            put(extra, "relerr_max", emax)
+            put(extra, "relerr_median", emed)
             del C1, C2
             if world == 1:
                 # a second, independent seed pair (A 123456, B 654321) beside the reference's A == B
@@ -583,7 +608,7 @@ def main():
                 G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B2, k, 0.0, C2o, m, N, fast, work, ct)
                 C1, C2 = G.dd_gemm(A, B2, m, n, k)
                 emax2, emed2 = G.relerr_dd(C2o, C1, C2)
-                extra["relerr_seed_pair_123456_654321"] = {"max": emax2, "median": emed2}
+                put(extra, "relerr_seed_pair_123456_654321", {"max": emax2, "median": emed2})
                 del C1, C2, B2, C2o
 
     if sharded and not args.no_single_gpu:
@@ -606,16 +631,16 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             single_ms = e0.elapsed_time(e1) / reps
-            extra["single_gpu_ms"] = round(single_ms, 4)
-            extra["single_gpu_tflops"] = round(flop_per / (single_ms * 1e-3) / 1e12, 2)
-            extra["strong_scaling_efficiency"] = round(single_ms / (world * ms_per_step), 4)
+            put(extra, "single_gpu_ms", round(single_ms, 4))
+            put(extra, "single_gpu_tflops", round(flop_per / (single_ms * 1e-3) / 1e12, 2))
+            put(extra, "strong_scaling_efficiency", round(single_ms / (world * ms_per_step), 4))
             del w1, C1g
             torch.cuda.empty_cache()
         barrier(world)
 
     if sharded and kind == "d" and not args.no_variants:
         # last of the collective phases: each variant is a phase of its own for the watchdog
-        extra["variants"] = {}
+        put(extra, "variants", {})
         time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops,
                       arm=lambda name: arm(f"variants: {name}", soft), out=extra["variants"])
 
@@ -626,8 +651,8 @@ def main():
         # any int8 GEMM on such data
         ceiling = G.mfma_ceiling()
         if ceiling > 0:
-            roofline["data_bound_ceiling"] = round(ceiling, 1)
-            roofline["frac_of_data_bound_ceiling"] = round(achieved / ceiling, 4)
+            put(roofline, "data_bound_ceiling", round(ceiling, 1))
+            put(roofline, "frac_of_data_bound_ceiling", round(achieved / ceiling, 4))
         if not args.no_dgemm and kind == "d" and (world == 1 or sharded):
             # the vendor DGEMM of the same shape on ONE GPU (rocBLAS through torch)
             Ar, Br = A.t(), B.t()
@@ -640,11 +665,18 @@ def main():
                 torch.matmul(Ar, Br)
             torch.cuda.synchronize()
             dg = 2.0 * m * n * k * reps / (time.perf_counter() - t1) / 1e12
-            extra["rocblas_dgemm_tflops_1gpu"] = round(dg, 2)
-            extra["vs_rocblas_dgemm_1gpu"] = round(value / dg, 3)
+            put(extra, "rocblas_dgemm_tflops_1gpu", round(dg, 2))
+            put(extra, "vs_rocblas_dgemm_1gpu", round(value / dg, 3))
         gpu_C = C if (world == 1 and kind == "d" and fast and N == 14) else None
-        report["cpu"] = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev, gpu_C)
-        print(json.dumps(line()), flush=True)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev, gpu_C, args.cpu_threads)
+        put(report, "cpu", cpu)
+        if wd:
+            # no fire between here and the print: a fire already in progress ends the process inside disarm()
+            # (the watchdog holds its lock while it reports), so exactly one line is printed either way
+            wd.disarm()
+        with STATE_LOCK:
+            text = json.dumps(line())
+        print(text, flush=True)
     if world > 1:
         import torch.distributed as dist
         arm("teardown", lambda msg: None)  # the line is out (rank 0) or not this rank's to print

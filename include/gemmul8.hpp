@@ -19,7 +19,10 @@
 //     returns {0,0,0,0} without touching C.
 // Differences (deliberate): all work is enqueued on the hipBLAS handle's stream
 // (null stream when handle == nullptr) with no device-wide synchronisation; the
-// call waits only for its own last event to fill the timers.  alpha/beta follow
+// call waits only for its own last event to fill the timers.  With the environment
+// variable GEMMUL8_TIMERS=0 (read once per process) it does not wait at all and
+// returns {0,0,0,0}: the call is then asynchronous on that stream, as the C ABI's
+// gemmul8_gemm with phase_ns = NULL.  alpha/beta follow
 // BLAS semantics for every value (the reference mis-applies some).
 // num_moduli outside [2, 20] or k beyond the int32-exact bound is rejected.
 #pragma once

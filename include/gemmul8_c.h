@@ -130,9 +130,16 @@ int gemmul8_recombine_cols(void *stream, size_t m, size_t n, size_t k, unsigned 
  * sums = column-major double [2][n][lds] (plane 0: C1 = sum hi_i r_i, plane 1: C2 = sum lo_i r_i; one-level
  * moduli, N <= 7 or float output: C1 = sum NMi_i r_i, C2 = 0) -- inverse_scaling.hpp:35-62, 138-172
  * restricted to the range.  The element-wise sums of all ranks' planes (an RCCL sum reduce) finish into C with
- * gemmul8_crt_finish (sftA / sftB from `work`).  C1 is exact in any order; C2 is a rounded sum whose order the
- * reduce changes, so C is within a few ulp of gemmul8_gemm's, not bit-identical.  Real outputs only
- * (GEMMUL8_E_UNSUPPORTED for complex compute types). */
+ * gemmul8_crt_finish (sftA / sftB from `work`).  Not bit-identical to gemmul8_gemm; how close depends on the
+ * moduli level:
+ *   two-level (f64 output, N >= 8): C1 is exact in any order, only C2's rounded sum is reordered: C within a
+ *     few ulp, max |C - C_gemm| <= 2^-40 max |C_gemm| in the tests;
+ *   one-level, N <= 5 (f64): every partial sum stays below 2^53, so C1 is exact: the same few-ulp bound;
+ *   one-level, N = 6, 7 (f64): C1 = sum NMi_i r_i exceeds 2^53 and is rounded in whatever order the reduce
+ *     takes (the single call's own C carries an error of that size): max |C - C_gemm| <= 2^-26 max |C_gemm|;
+ *   float output (one-level at every N): the same reordering, then the rounding to float:
+ *     max |C - C_gemm| <= 2^-19 max |C_gemm|.
+ * Real outputs only (GEMMUL8_E_UNSUPPORTED for complex compute types). */
 int gemmul8_crt_partial(void *stream, size_t m, size_t n, size_t k, unsigned num_moduli, int type_c,
                         int compute_type, const void *work, unsigned mod_begin, unsigned mod_end, double *sums,
                         size_t lds);

@@ -866,6 +866,18 @@ static int op_code(hipblasOperation_t op) {
     return op == HIPBLAS_OP_N ? GEMMUL8_OP_N : (op == HIPBLAS_OP_T ? GEMMUL8_OP_T : GEMMUL8_OP_C);
 }
 
+// GEMMUL8_TIMERS=0: gemmul8::gemm returns {0,0,0,0} without waiting for its kernels (the call is then as
+// asynchronous as gemmul8_gemm with phase_ns = NULL: everything is enqueued on the handle's stream); unset or
+// any other value: the reference's contract, phase times in ns, the call returning after its own completion
+// (gemmul8.hpp:24-28).  Read once per process.
+static bool cxx_timers() {
+    static const bool on = [] {
+        const char *e = getenv("GEMMUL8_TIMERS");
+        return !(e && e[0] == '0' && e[1] == 0);
+    }();
+    return on;
+}
+
 template <typename TA, typename TB, typename TC>
 static std::vector<double> gemm_impl(hipblasHandle_t handle, hipblasOperation_t op_A, hipblasOperation_t op_B,
                                      size_t m, size_t n, size_t k, const TC *alpha, const TA *A, size_t lda,
@@ -876,7 +888,7 @@ static std::vector<double> gemm_impl(hipblasHandle_t handle, hipblasOperation_t 
     if (handle) (void)hipblasGetStream(handle, &st);
     const int rc = gemmul8_gemm(st, op_code(op_A), op_code(op_B), m, n, k, dtype_of<TA>::v, dtype_of<TB>::v,
                                 dtype_of<TC>::v, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fastmode ? 1 : 0,
-                                work, (int)computeType, timer.data());
+                                work, (int)computeType, cxx_timers() ? timer.data() : nullptr);
     if (rc == GEMMUL8_E_TYPES) fprintf(stderr, "Unsupported compute type for the argument types.\n");
     else if (rc != GEMMUL8_OK) fprintf(stderr, "gemmul8::gemm: invalid arguments or unsupported mode (code %d)\n", rc);
     if (rc != GEMMUL8_OK) return std::vector<double>(4, 0.0);

@@ -219,13 +219,29 @@ def crt_partial(m, n, k, num_moduli, out_dtype, work, mod_begin, mod_end, sums, 
     """Partial CRT sums of moduli [mod_begin, mod_end) into `sums` (float64 tensor (2, n, m): C1 then C2,
     column-major planes; real outputs).  The element-wise sums of the partials of a moduli partition
     finish with crt_finish (include/gemmul8_c.h: C1 exact, C2 rounded in the summation order)."""
-    assert sums.dtype == torch.float64 and sums.numel() >= 2 * n * m
+    _check_sums(sums, m, n)
     _check(lib.gemmul8_crt_partial(_stream(stream), m, n, k, num_moduli, _DTYPE[out_dtype], REAL_DEFAULT,
                                    work.data_ptr(), mod_begin, mod_end, sums.data_ptr(), m))
 
 
+def _check_sums(sums, m, n):
+    """the partial-sum planes the native kernels index as double [2][n][m] (lds = m)"""
+    if sums.dtype != torch.float64:
+        raise TypeError(f"partial CRT sums must be float64, not {sums.dtype}")
+    if not sums.is_contiguous():
+        raise ValueError("partial CRT sums must be contiguous (column-major [2][n][m] planes)")
+    if sums.numel() < 2 * n * m:
+        raise ValueError(f"partial CRT sums hold {sums.numel()} doubles, need 2 * n * m = {2 * n * m}")
+
+
 def crt_finish(m, n, k, num_moduli, alpha, beta, C, ldc, work, sums, stream=None):
     """C = alpha * CRT(summed partials) scaled by the workspace's shifts + beta * C (real outputs)."""
+    _check_sums(sums, m, n)
+    if C.dtype not in (torch.float64, torch.float32):
+        raise TypeError(f"crt_finish: C must be float64 or float32, not {C.dtype}")
+    if ldc < m or not C.is_contiguous() or C.numel() < ldc * (n - 1) + m:
+        raise ValueError(f"crt_finish: C (numel {C.numel()}, contiguous {C.is_contiguous()}) does not hold a "
+                         f"column-major {m} x {n} matrix with ldc = {ldc}")
     al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
     _check(lib.gemmul8_crt_finish(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], REAL_DEFAULT, al.ptr, be.ptr,
                                   C.data_ptr(), ldc, work.data_ptr(), sums.data_ptr(), m))

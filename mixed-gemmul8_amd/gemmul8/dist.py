@@ -623,11 +623,19 @@ def gemm_moduli_reduce(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmod
     """The north star's partition (BASELINE.json): whole moduli per rank (moduli_partition: 14 over 8 ranks
     2,2,2,2,2,2,1,1), every rank its own shifts, residue planes and partial CRT sums (C1, C2) of its moduli, ONE
     RCCL sum-reduce of the two FP64 m x n planes to the root, and the root's finishing CRT (include/gemmul8_c.h
-    gemmul8_crt_partial / gemmul8_crt_finish).  Real outputs, alpha = 1, beta = 0.  C1 sums exactly in any order;
-    C2 is a rounded sum whose order the reduce changes, so C is within a few ulp of the single call's but not
-    bit-identical, and the reduce moves 16 B per element per rank (4.3 GB at cfg3) against gemm_moduli's residue
-    exchange (N m n / W bytes received per rank, 0.47 GB).  Kept for comparison (bench.py times it).  Returns C
-    (n, m) on the root, None elsewhere."""
+    gemmul8_crt_partial / gemmul8_crt_finish).  Real outputs, alpha = 1, beta = 0.  Not bit-identical to the
+    single call; the bound depends on the moduli level (include/gemmul8_c.h): two-level moduli (f64 output,
+    N >= 8) and f64 N <= 5 sum C1 exactly in any order, only C2's rounded sum is reordered (C within 2^-40 of
+    max |C|); f64 N = 6, 7 round C1 = sum NMi_i r_i beyond 2^53 in the reduce's order (within 2^-26 of max |C|);
+    float output is one-level at every N (within 2^-19 of max |C|).  The reduce moves 16 B per element per rank
+    (4.3 GB at cfg3) against gemm_moduli's residue exchange (N m n / W bytes received per rank, 0.47 GB).  Kept
+    for comparison (bench.py times it).  Returns C (n, m) on the root, None elsewhere."""
+    # argument errors before any collective is posted (a failure inside the native calls could leave the
+    # other ranks waiting in the reduce)
+    if A.is_complex() or B.is_complex():
+        raise ValueError("gemm_moduli_reduce: real operands only (the partial CRT sums have no complex form)")
+    if out_dtype is not None and out_dtype not in (torch.float32, torch.float64):
+        raise ValueError(f"gemm_moduli_reduce: out_dtype must be float32 or float64, not {out_dtype}")
     ops = ops or _shard_ops()
     out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
     rank, world = _group_info(group)

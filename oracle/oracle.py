@@ -34,6 +34,8 @@ def lib():
         _lib.oz2o_gemm.argtypes = [c, c, c, i, i, sz, sz, sz, p, p, sz, p, sz, p, p, sz, u, i, i, i, p, p, i]
         _lib.oz2o_vnni.restype = i
         _lib.oz2o_vnni.argtypes = []
+        _lib.oz2o_set_num_threads.argtypes = [i]
+        _lib.oz2o_set_num_threads.restype = None
     return _lib
 
 
@@ -127,6 +129,11 @@ def gemm(A, B, num_moduli, fastmode=True, out_dtype=None, alpha=1.0, beta=0.0, C
 
 def num_threads():
     return lib().oz2o_num_threads()
+
+
+def set_num_threads(n):
+    """OpenMP team size of later oracle calls (the bench's CPU baseline; n <= 0: unchanged)"""
+    lib().oz2o_set_num_threads(int(n))
 
 
 def vnni():

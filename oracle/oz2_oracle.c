@@ -769,3 +769,12 @@ int oz2o_num_threads(void) {
     return 1;
 #endif
 }
+
+/* bench.py --cpu-threads: the OpenMP team size of later calls (n <= 0 leaves it unchanged) */
+void oz2o_set_num_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
+}

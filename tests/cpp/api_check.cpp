@@ -35,7 +35,55 @@ static double rnd(unsigned &s) {
     return ((s >> 8) / 16777216.0 - 0.5) * (1.0 + (s & 7));
 }
 
-int main() {
+// GEMMUL8_TIMERS=0 (run with argv[1] == "async"): gemmul8::gemm returns {0,0,0,0} before its kernels finish;
+// otherwise (the default contract) it returns after them.  Two back-to-back calls, bits against the C ABI.
+static int check_async(hipblasHandle_t h, hipStream_t st, bool async) {
+    const size_t s = 4096;  // ~1.5 ms of GPU work per call: the enqueue returns long before that
+    const unsigned N = 14;
+    unsigned seed = 11;
+    std::vector<double> hA(s * s), hC(s * s, 0.0);
+    for (auto &x : hA) x = rnd(seed);
+    double *A = upload(hA), *C = upload(hC), *C3 = upload(hC), *Cr = upload(hC);
+    void *work;
+    CHECK(hipMalloc(&work, gemmul8::workSize(s, s, s, N)) == hipSuccess);
+    const double one = 1.0, zero = 0.0;
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+    std::vector<double> t1 = gemmul8::gemm<double>(h, HIPBLAS_OP_N, HIPBLAS_OP_N, s, s, s, &one, A, s, A, s, &zero, C, s,
+                                                   N, true, work);
+    std::vector<double> t2 = gemmul8::gemm<double>(h, HIPBLAS_OP_N, HIPBLAS_OP_T, s, s, s, &one, A, s, A, s, &zero, C3,
+                                                   s, N, true, work);
+    const hipError_t q = hipStreamQuery(st);  // right after the second call returned
+    if (async) {
+        CHECK(q == hipErrorNotReady);  // its kernels were still queued or running
+        CHECK(t1 == std::vector<double>(4, 0.0) && t2 == std::vector<double>(4, 0.0));
+    } else {
+        CHECK(q == hipSuccess);  // the synchronous contract: the call waited for its own completion
+        CHECK(t1[1] > 0.0 && t2[1] > 0.0);
+    }
+    CHECK(hipStreamSynchronize(st) == hipSuccess);
+    CHECK(gemmul8_gemm(st, GEMMUL8_OP_N, GEMMUL8_OP_N, s, s, s, GEMMUL8_R_64F, GEMMUL8_R_64F, GEMMUL8_R_64F, &one, A, s, A,
+                       s, &zero, Cr, s, N, 1, work, GEMMUL8_REAL_DEFAULT, nullptr) == GEMMUL8_OK);
+    CHECK(hipStreamSynchronize(st) == hipSuccess);
+    CHECK(download(C, s * s) == download(Cr, s * s));
+    CHECK(gemmul8_gemm(st, GEMMUL8_OP_N, GEMMUL8_OP_T, s, s, s, GEMMUL8_R_64F, GEMMUL8_R_64F, GEMMUL8_R_64F, &one, A, s, A,
+                       s, &zero, Cr, s, N, 1, work, GEMMUL8_REAL_DEFAULT, nullptr) == GEMMUL8_OK);
+    CHECK(hipStreamSynchronize(st) == hipSuccess);
+    CHECK(download(C3, s * s) == download(Cr, s * s));
+    CHECK(hipFree(A) == hipSuccess && hipFree(C) == hipSuccess && hipFree(C3) == hipSuccess && hipFree(Cr) == hipSuccess);
+    CHECK(hipFree(work) == hipSuccess);
+    std::printf("%s OK\n", async ? "async" : "sync");
+    return 0;
+}
+
+int main(int argc, char **argv) {
+    if (argc > 1 && (std::strcmp(argv[1], "async") == 0 || std::strcmp(argv[1], "sync") == 0)) {
+        hipStream_t st;
+        CHECK(hipStreamCreate(&st) == hipSuccess);
+        hipblasHandle_t h;
+        CHECK(hipblasCreate(&h) == HIPBLAS_STATUS_SUCCESS);
+        CHECK(hipblasSetStream(h, st) == HIPBLAS_STATUS_SUCCESS);
+        return check_async(h, st, std::strcmp(argv[1], "async") == 0);
+    }
     const size_t m = 300, n = 260, k = 513;
     const unsigned N = 14;
     unsigned seed = 7;

@@ -2,7 +2,7 @@
 (ranks as threads on one GPU): shapes, moduli counts, rank counts 2..5, fast / accurate, real / complex (with
 Karatsuba products), unit orders, side stream on / off, C gathered or distributed, random transfer delays, two
 calls per case through the same workspaces.  Every rank's output is compared bit for bit with the single
-gemmul8_gemm call.  Used by tests/test_gpu_dist_streams.py (a short run) and tools/probes/fake_nccl_soak.py."""
+gemmul8_gemm call.  Used by tests/test_gpu_dist_streams.py (a short run); long soaks: python tests/dist_soak.py [cases] [seed]."""
 import os
 
 import numpy as np
@@ -85,3 +85,16 @@ def soak(cases, seed, log=None):
         if log and (i + 1) % 10 == 0:
             log(f"{i + 1} cases, {len(fails)} failures")
     return len(fails), fails
+
+
+if __name__ == "__main__":
+    import sys
+    import time
+    cases = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    t0 = time.time()
+    n, fails = soak(cases, seed, log=lambda s: print(f"{s}, {time.time() - t0:.0f} s", flush=True))
+    for c, msg in fails:
+        print("FAIL", c, msg, flush=True)
+    print(f"done: {cases} cases, {n} failures, {time.time() - t0:.0f} s")
+    sys.exit(1 if n else 0)

@@ -23,3 +23,22 @@ def test_cpp_api_drop_in(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
+def test_cpp_api_async_switch(tmp_path):
+    """GEMMUL8_TIMERS=0: gemmul8::gemm returns {0,0,0,0} while its kernels are still queued (hipStreamQuery right
+    after two back-to-back 4096^3 calls reports not ready); without it the call returns after its own completion
+    with phase times.  Both runs bit-identical to the C ABI."""
+    exe = str(tmp_path / "api_check")
+    cmd = ["/opt/rocm/bin/hipcc", "-std=c++20", "-O1", "-I" + os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "cpp", "api_check.cpp"), "-L" + LIBDIR, "-lgemmul8_amd", "-lhipblas",
+           "-Wl,-rpath," + LIBDIR, "-o", exe]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    env = dict(os.environ)
+    env["GEMMUL8_TIMERS"] = "0"
+    r = subprocess.run([exe, "async"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "async OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    env.pop("GEMMUL8_TIMERS")
+    r = subprocess.run([exe, "sync"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0 and "sync OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])

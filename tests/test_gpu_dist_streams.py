@@ -185,7 +185,7 @@ def test_row_blocks_accurate_gathered(monkeypatch):
 
 
 def test_random_cases():
-    """40 random cases of the NCCL branch (tests/dist_soak.py; tools/probes/fake_nccl_soak.py runs hundreds)"""
+    """40 random cases of the NCCL branch (tests/dist_soak.py; its command line runs hundreds)"""
     from dist_soak import soak
     n, fails = soak(40, 2024)
     assert n == 0, fails[:3]

@@ -1,6 +1,7 @@
 #!/bin/bash
 # One gpurun session of checks: usage tools/gpu_session.sh <tag> <step>...
-#   steps: tests=<pytest args>   golden_cfg1   bench=<bench args>   gloo2=<bench args>
+#   steps: tests=<pytest args>   golden_cfg1   bench=<bench args>   gloo2|gloo4|gloo8=<bench args>
+#          profile=<tag + bench args>   cmd=<shell command>
 # Every GPU step runs under its own time limit; the first failure ends the session.
 set -o pipefail
 TAG=$1
@@ -31,6 +32,10 @@ for step in "$@"; do
     gloo4)
       GEMMUL8_BENCH_BACKEND=gloo timeout -k 10 300 python bench.py --gpus 4 $arg > $OUT/gloo4_$i.json 2> $OUT/gloo4_$i.err
       rc=$?; cat $OUT/gloo4_$i.json ;;
+    gloo8)
+      # the driver's 8-rank bench rehearsed on one GPU (gloo, ranks sharing the device; timing meaningless)
+      GEMMUL8_BENCH_BACKEND=gloo timeout -k 10 900 python bench.py --gpus 8 $arg > $OUT/gloo8_$i.json 2> $OUT/gloo8_$i.err
+      rc=$?; cat $OUT/gloo8_$i.json ;;
     profile)
       timeout -k 10 900 bash tools/profile.sh $arg > $OUT/profile_$i.log 2>&1
       rc=$?; tail -5 $OUT/profile_$i.log ;;
