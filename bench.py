@@ -326,6 +326,15 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lam
     timed(f"output_blocks_{R}x{Q}_all_moduli", blk)
     if fast and a1 > a0 and b1 > b0:
         del wb, Cb
+    # the 2-D unit grid (gemm_moduli_grid): two row blocks of W / 2 ranks, each a (modulus, column block)
+    # partition of its rows over its own sub-group -- each rank reads half of A and exchanges within its row block
+    if fast and world >= 4 and world % 2 == 0:
+        gops = GD.HipShardOps()
+        timed(f"moduli_grid_2x{world // 2}",
+              lambda: GD.gemm_moduli_grid(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, row_blocks=2,
+                                          ops=gops, order=args.order))
+        GD.release_workspaces(gops)
+        torch.cuda.empty_cache()
     # the north star's partition as built (gemm_moduli_reduce): whole moduli per rank, partial FP64 CRT sums,
     # one sum-reduce of the two m x n planes to the root, the root's finishing CRT (C within ulps, not bit-identical)
     timed("moduli_partial_sums_reduce",

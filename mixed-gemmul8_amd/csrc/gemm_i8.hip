@@ -575,7 +575,8 @@ constexpr unsigned NO_TILE = 0xffffffffu;
 
 struct TileRef {
     unsigned j, sb, tm, tn;
-    uint32_t offA, offB;  // byte offsets of the tile's k-step 0 panel in its modulus's A and B planes
+    uint32_t offA, offB;  // byte offsets of the tile's first staged k-step panel in its modulus's A and B planes
+    uint32_t step;        // byte step of the DMA cursor from one k-step to the next (PANEL, or -PANEL mod 2^32)
 };
 
 template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArgs &g, unsigned u) {
@@ -614,7 +615,11 @@ template <bool SUB> __device__ __forceinline__ TileRef decode_tile(const GemmArg
 #ifndef OZ2_STAMPS
 #define OZ2_STAMPS 0  // probe builds only (tools/probes/persist_stamps.hip): s_memtime phase sums per wave
 #endif
-template <bool SUB, int PRIO = 1, int EPIM = 0>
+// ORD (A/B probes): 0 = every tile walks k ascending (default); 1 = serpentine: the tiles of every other round of
+// a queue (queue position / blocks per queue odd) walk k descending, so a round's first k-steps read the A panels
+// its predecessor round (same row tiles, the next column tiles) read last, while they may still sit in the XCD's
+// L2.  Integer sums in any order: identical residues.
+template <bool SUB, int PRIO = 1, int EPIM = 0, int ORD = 0>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArgs g) {
 #if OZ2_STAMPS
     // [0] realign, [1] residues -> LDS, [2] park barrier, [3] stores + barrier, [4] accumulator reset +
@@ -674,22 +679,33 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
     auto lo_of = [&](unsigned step) { return lds_wave + (step & (PSTAGES - 1)) * SLOT; };
     auto rd_of = [&](unsigned step) { return smem + (step & (PSTAGES - 1)) * SLOT; };
 
-    TileRef ct = decode_tile<SUB>(g, tile_u(ccur));
+    auto ref_of = [&](unsigned pos) {  // the tile at queue position pos, with its k direction
+        TileRef t = decode_tile<SUB>(g, tile_u(pos));
+        t.step = PANEL;
+        if (ORD == 1 && ((pos / nblk) & 1u)) {
+            t.offA += (K - 1) * PANEL;
+            t.offB += (K - 1) * PANEL;
+            t.step = 0u - (uint32_t)PANEL;
+        }
+        return t;
+    };
+    TileRef ct = ref_of(ccur);
     v4si rA = rsrcA(ct), rB = rsrcB(ct);  // descriptors of the DMA cursor
+    uint32_t cstep = ct.step;             // and its step
     constexpr unsigned D = PSTAGES - 1;
     for (unsigned s0 = 0; s0 < D; ++s0) {  // steps 0..2 of the first tile
         const uint32_t lo = lo_of(s0);
-        bglds16(rA, ct.offA + s0 * PANEL + lane_off, lo);
-        bglds16(rA, ct.offA + s0 * PANEL + lane_off + 8192, lo + 8192);
-        bglds16(rB, ct.offB + s0 * PANEL + lane_off, lo + PANEL);
-        bglds16(rB, ct.offB + s0 * PANEL + lane_off + 8192, lo + PANEL + 8192);
+        bglds16(rA, ct.offA + s0 * cstep + lane_off, lo);
+        bglds16(rA, ct.offA + s0 * cstep + lane_off + 8192, lo + 8192);
+        bglds16(rB, ct.offB + s0 * cstep + lane_off, lo + PANEL);
+        bglds16(rB, ct.offB + s0 * cstep + lane_off + 8192, lo + PANEL + 8192);
     }
     wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();  // step 0 landed (and the claim's LDS write)
     barrier();
 
     unsigned s = 0;                                             // global k-step of this block (slot s mod 4)
     unsigned cnext = __builtin_amdgcn_readfirstlane(spare[0]);  // the tile after the current one
-    uint32_t da = ct.offA + D * PANEL, db = ct.offB + D * PANEL;  // DMA cursor: panels of the next step staged
+    uint32_t da = ct.offA + D * cstep, db = ct.offB + D * cstep;  // DMA cursor: panels of the next step staged
     Frags f;
     AccTile acc[ACC_I][ACC_J];
     for (unsigned r = 0;; ++r) {
@@ -701,7 +717,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
         if (wr == 1) barrier();  // group 1 falls one barrier behind (ping-pong, as in the one-tile kernel)
         OZ2_STAMP(4);
         unsigned k = 0;
-        uint32_t na = 0, nb = 0;  // the next tile's step-0 panels
+        uint32_t na = 0, nb = 0, nstep = PANEL;  // the next tile's first panels and its step
         v4si nrA = rA, nrB = rB;  // and its descriptors
         // one k-step: reads of slot s, DMA of step s+3 (this tile's step k+3, or the next tile's step
         // k+3-K once k+3 >= K: the cursor jumps there after staging this tile's last step), wait, MFMAs
@@ -714,11 +730,12 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             bglds16(rB, db + lane_off, lo + PANEL);
             bglds16(rB, db + lane_off + 8192, lo + PANEL + 8192);
             const bool jump = k + D + 1 == K;
-            da = jump ? na : da + PANEL;
-            db = jump ? nb : db + PANEL;
+            da = jump ? na : da + cstep;
+            db = jump ? nb : db + cstep;
             if (jump) {  // block-uniform
                 rA = nrA;
                 rB = nrB;
+                cstep = nstep;
             }
             wait();
             barrier();
@@ -737,9 +754,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
         }
         TileRef nt = ct;
         if (cnext != NO_TILE) {
-            nt = decode_tile<SUB>(g, tile_u(cnext));
+            nt = ref_of(cnext);
             na = nt.offA;
             nb = nt.offB;
+            nstep = nt.step;
             nrA = rsrcA(nt);
             nrB = rsrcB(nt);
         }
@@ -933,6 +951,7 @@ std::atomic<int> g_last_residue_kernel{0};
 int g_persistent_override = -1;
 int g_prio_override = 1;  // probes: the persistent kernel's priority variant (PRIO; 1 = the default)
 int g_epim_override = 0;  // probes: the persistent kernel's residue arithmetic (EPIM; 0 = the default)
+int g_order_override = 0;  // probes: the persistent kernel's k order (ORD; 0 = the default)
 unsigned long long *g_stamps = nullptr;  // probes: OZ2_STAMPS builds' per-wave phase sums
 static int persistent_mode() {
     if (g_persistent_override >= 0) return g_persistent_override;
@@ -1030,6 +1049,9 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
 #ifdef OZ2_EPIM_PROBES
         else if (g_epim_override == 3) launch(gemm_i8_persistent_kernel<false, 1, 3>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 4) launch(gemm_i8_persistent_kernel<false, 1, 4>, pgrid, dim3(NTHREADS), st, g);
+#endif
+#ifdef OZ2_ORDER_PROBES
+        else if (g_order_override == 1) launch(gemm_i8_persistent_kernel<false, 1, 0, 1>, pgrid, dim3(NTHREADS), st, g);
 #endif
         else if (g_prio_override == 0) launch(gemm_i8_persistent_kernel<false, 0>, pgrid, dim3(NTHREADS), st, g);
         else if (g_prio_override == 2) launch(gemm_i8_persistent_kernel<false, 2>, pgrid, dim3(NTHREADS), st, g);

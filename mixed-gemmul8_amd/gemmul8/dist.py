@@ -32,6 +32,10 @@ results bit-identical to the single-GPU ``gemmul8.gemm`` on the same inputs.
     sums (which would also reorder the double-double low-word sum) or 3.2 GB into one root for
     gathering the planes there.
 
+``gemm_moduli_grid``   (the 2-D unit grid: moduli x row blocks x column blocks; fast mode)
+    H row blocks of G = W / H ranks, each row block a gemm_moduli over its own sub-group: a rank reads 1/H
+    of op(A) instead of all of it and exchanges residues with the G - 1 ranks of its row block only.
+
 ``matmul_rows``    rank r owns a row block of C = A @ B and computes every modulus for it
     from its own rows of A and the full (replicated) B.  The shift of a row of A depends only
     on that row and the shifts of B's columns only on B, so the block equals the matching rows
@@ -71,7 +75,7 @@ from . import (OP_N, OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, 
 __all__ = ["OP_N", "OP_T", "REAL_DEFAULT", "COMPLEX_BIG_MATRIX_ENCODE", "ShardPlan", "HipShardOps", "HipOps", "blocks",
            "moduli_partition", "row_partition", "gemm_moduli", "gemm_moduli_planes_to_root", "matmul_moduli",
            "matmul_rows", "release_workspaces", "side_stream_enabled", "StageWatchdog", "progress",
-           "gemm_moduli_reduce"]
+           "gemm_moduli_reduce", "gemm_moduli_grid", "grid_groups"]
 
 TILE = 256  # product tile edge: column blocks of the product units start at multiples of it
 WORKSPACE_CACHE = 2  # workspaces (shapes) kept per native ops object
@@ -662,6 +666,92 @@ def gemm_moduli_reduce(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmod
         return None
     C = ops.finish(st, S)
     progress("done")
+    return C
+
+
+_GRID_GROUPS = {}
+
+
+def grid_groups(world, row_blocks, group=None):
+    """The sub-groups of gemm_moduli_grid: row block h owns the ranks [h G, (h + 1) G) of `group`, G = W / H.
+    Created once per (group, W, H); dist.new_group is collective, so every rank of `group` creates all of them,
+    in the same order."""
+    key = (id(group), world, row_blocks)
+    if key not in _GRID_GROUPS:
+        G = world // row_blocks
+        ranks = [_global(group, r) for r in range(world)]
+        _GRID_GROUPS[key] = [dist.new_group(ranks[h * G:(h + 1) * G]) for h in range(row_blocks)]
+    return _GRID_GROUPS[key]
+
+
+def gemm_moduli_grid(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
+                     computeType=REAL_DEFAULT, group=None, row_blocks=2, gather=False, root=0, ops=None,
+                     align=TILE, order="moduli"):
+    """The 2-D unit grid (moduli x row blocks x column blocks): the W ranks form H row blocks of G = W / H ranks;
+    the ranks of row block h run gemm_moduli on its rows of op(A) (rows blocks(m, H)[h], B replicated) over their
+    own sub-group, i.e. (modulus, column block) units of that row block and the residue exchange among those G
+    ranks only.  A rank's encode reads 1/H of op(A) instead of all of it (gemm_moduli: every rank reads all rows
+    of op(A), 2.15 GB of its 4.3 GB at cfg3, W = 8), its exchange stays inside its row block (G - 1 peers), and
+    each rank still multiplies 1/W of the MACs.  Fast-mode shifts depend on one row or column each, so every
+    block is bit-identical to the single call's.  Fast mode only: the accurate-mode column shifts of op(B) come
+    from the bound product over ALL rows of op(A), a reduction across row blocks gemm_moduli does not make.
+
+    Returns this rank's block -- rows blocks(m, H)[h], columns ShardPlan(m_h, n, N, G).cols[rank % G] -- as a
+    (c1 - c0, m_h) tensor (column-major), or with gather=True the whole (n, m) C on the root and None
+    elsewhere.  A, B: column-major storage as in gemm_moduli (op N: an (k, m) tensor; op T: an (m, k) one)."""
+    if not fastmode:
+        raise ValueError("gemm_moduli_grid: fast mode only (accurate-mode column shifts span every row block)")
+    rank, world = _group_info(group)
+    if row_blocks < 1 or world % row_blocks:
+        raise ValueError(f"gemm_moduli_grid: {row_blocks} row blocks do not divide {world} ranks")
+    if gather and root != 0:
+        raise ValueError("gemm_moduli_grid: gather=True collects C on rank 0 of the group")
+    out_dtype = out_dtype or torch.promote_types(A.dtype, B.dtype)
+    G = world // row_blocks
+    h, sub = divmod(rank, G)
+    rblocks = blocks(m, row_blocks, align)
+    r0, r1 = rblocks[h]
+    subgroups = grid_groups(world, row_blocks, group)
+    # rows [r0, r1) of op(A): a column range of op(A)'s storage for op N (column-major m x k: the (k, m) tensor's
+    # second index), a row range of the (m, k) tensor for op T / C
+    Ah = A[:, r0:r1] if opA == OP_N else A[r0:r1]
+    mh = r1 - r0
+    if mh > 0:
+        Cb = gemm_moduli(opA, opB, mh, n, k, Ah, lda, B, ldb, num_moduli, fastmode, out_dtype, computeType,
+                         group=subgroups[h], gather=gather, root=0, ops=ops, align=align, order=order)
+    elif gather:  # (every rank of an empty row block skips, so its sub-group stays consistent)
+        Cb = torch.empty((n, 0), dtype=out_dtype, device=A.device) if sub == 0 else None
+    else:
+        Cb = torch.empty((0, 0), dtype=out_dtype, device=A.device)
+    if not gather:
+        return Cb
+    # the row blocks' roots (sub-group rank 0) hold their (n, m_h) blocks: to the global root
+    host_sync = dist.get_backend(group) != "nccl"
+    if host_sync and A.is_cuda:
+        torch.cuda.current_stream().synchronize()
+    groot = _global(group, root)
+    if sub != 0:
+        return None
+    if rank != root:
+        if mh > 0:
+            _send(Cb.contiguous(), groot, group)
+        return None
+    C = torch.empty((n, m), dtype=out_dtype, device=Cb.device)
+    bufs, rq = {}, []
+    for hh, (a, b) in enumerate(rblocks):
+        src = hh * G
+        if b <= a:
+            continue
+        if src == rank:
+            C[:, a:b] = Cb
+            continue
+        bufs[hh] = torch.empty((n, b - a), dtype=out_dtype, device=Cb.device)
+        rq.append(dist.P2POp(dist.irecv, bufs[hh], _global(group, src), group))
+    for q in (dist.batch_isend_irecv(rq) if rq else []):
+        q.wait()
+    for hh, buf in bufs.items():
+        a, b = rblocks[hh]
+        C[:, a:b] = buf
     return C
 
 

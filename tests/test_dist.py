@@ -195,6 +195,14 @@ def _worker(rank, world, port, case, outdir):
                 np.save(os.path.join(outdir, "reduce.npy"), Cr.t().contiguous().numpy())
             else:
                 assert Cr is None
+        # the 2-D unit grid: two row blocks, each a gemm_moduli over its own sub-group (fast mode, even W)
+        if fast and world % 2 == 0:
+            Cg = GD.gemm_moduli_grid(1, 1, m, n, k, torch.from_numpy(A), k, torch.from_numpy(B), n, N, fast,
+                                     ops=OracleShardOps(), row_blocks=2, gather=True, align=16, order=order)
+            if rank == 0:
+                np.save(os.path.join(outdir, "grid.npy"), Cg.t().contiguous().numpy())
+            else:
+                assert Cg is None
         # SURVEY 8(e) variant (i): whole moduli per rank, planes gathered on the root
         Cp = GD.gemm_moduli_planes_to_root(1, 1, m, n, k, torch.from_numpy(A), k, torch.from_numpy(B), n, N, fast,
                                            ops=OracleShardOps())
@@ -241,7 +249,8 @@ def test_sharded_equals_single_call(tmp_path, world, case):
     A = ((rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))).astype(dt)
     B = ((rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))).astype(dt)
     C = O.gemm(A, B, N, fast)
-    for name in ("moduli", "rows", "planes"):
+    names = ("moduli", "rows", "planes") + (("grid",) if fast and world % 2 == 0 else ())
+    for name in names:
         got = np.load(tmp_path / f"{name}.npy")
         assert got.shape == C.shape
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C).view(np.uint8)), name
