@@ -140,6 +140,12 @@ def dist_setup():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
             dist.init_process_group(backend, timeout=tmo)
+        if world >= 4 and world % 2 == 0 and os.environ.get("GEMMUL8_BENCH_NO_GRID") is None:
+            # the sub-groups of the 2-D grid variant, created now: the communication libraries announce new
+            # groups on fd 1 (gloo does), and stdout must carry rank 0's one JSON line only
+            sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd"))
+            from gemmul8 import dist as GD
+            GD.grid_groups(world, 2)
         dist.barrier()  # the connections are up before stdout is given back
         world = dist.get_world_size()
         rank = dist.get_rank()

@@ -97,6 +97,10 @@ def main():
     ap.add_argument("--period", type=float, default=0.01)
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--moduli", type=int, default=14)
+    ap.add_argument("--cfg", type=int, default=2, choices=[2, 4, 5],
+                    help="workload of the gemm / products loops: 2 (default), 4 (d x s -> d, N = 10, accurate) or 5 "
+                         "(complex 4096^3, N = 12, Karatsuba products)")
+    ap.add_argument("--no-calibration", action="store_true", help="skip the mfma / hbm_read / mall_read loops")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
 
@@ -114,16 +118,26 @@ def main():
     res = info["energy_count"].get("counter_resolution") if isinstance(info["energy_count"], dict) else None
     uj_per_count = float(res) if res else 15.259  # microjoules per accumulator count
 
+    d = torch.device("cuda", 0)
+    ta, tb, ct, fast = torch.float64, torch.float64, G.REAL_DEFAULT, True
     m = n = k = args.size
     N = args.moduli
-    d = torch.device("cuda", 0)
-    A = G.randmat(m, k, torch.float64, 0.5, 123456, d)
-    C = torch.empty((n, m), dtype=torch.float64, device=d)
-    work = G.alloc_work(m, n, k, N, G.REAL_DEFAULT, d)
-    gemm = lambda: G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, A, k, 0.0, C, m, N, True, work)
-    prods = lambda: G.products(m, n, k, N, work)
-    big = torch.ones(512 * 1024 * 1024, dtype=torch.float64, device=d)       # 4 GiB
-    mall = torch.ones(16 * 1024 * 1024, dtype=torch.float64, device=d)       # 128 MiB
+    if args.cfg == 4:
+        tb, N, fast = torch.float32, 10, False
+    elif args.cfg == 5:
+        ta = tb = torch.complex128
+        ct, N, m = G.COMPLEX_BIG_MATRIX_ENCODE, 12, 4096
+        n = k = m
+    A = G.randmat(m, k, ta, 0.5, 123456, d)
+    B = A if tb == ta else G.randmat(k, n, tb, 0.5, 123456, d)
+    C = torch.empty((n, m), dtype=ta, device=d)
+    work = G.alloc_work(m, n, k, N, ct, d)
+    gemm = lambda: G.gemm(G.OP_N, G.OP_N, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, work, ct)
+    prods = lambda: G.products(m, n, k, N, work, computeType=ct)
+    L = G.layout(m, n, k, N, ct)
+    fmac = (3.0 if L["nsub"] == 3 else 4.0) if args.cfg == 5 else 1.0
+    big = torch.ones(512 * 1024 * 1024 if not args.no_calibration else 1, dtype=torch.float64, device=d)  # 4 GiB
+    mall = torch.ones(16 * 1024 * 1024 if not args.no_calibration else 1, dtype=torch.float64, device=d)  # 128 MiB
     for f in (gemm, prods, lambda: big.sum(), lambda: mall.sum()):
         f()
     torch.cuda.synchronize()
@@ -153,17 +167,22 @@ def main():
         sampler.phase = "gap"
         time.sleep(0.3)
 
-    ops = 2.0 * m * n * k * N
+    ops = 2.0 * fmac * m * n * k * N
     sampler.phase = "idle"
     t0 = time.perf_counter()
     time.sleep(args.seconds)
     phases["idle"] = {"t0": t0, "t1": time.perf_counter(), "calls": 0}
-    run("gemm", gemm, {"int8_ops": ops, "emulated_flop": 2.0 * m * n * k})
+    run("gemm", gemm, {"int8_ops": ops + (0 if fast else 2.0 * fmac * m * n * k),
+                       "emulated_flop": (8.0 if args.cfg == 5 else 2.0) * m * n * k})
     run("products", prods, {"int8_ops": ops})
-    iters = 100000
-    run("mfma", lambda: G.mfma_ceiling(iters), {"note": "two launches of each MFMA form per call"})
-    run("hbm_read", lambda: big.sum(), {"bytes": big.numel() * 8})
-    run("mall_read", lambda: mall.sum(), {"bytes": mall.numel() * 8})
+    if not args.no_calibration:
+        iters = 100000
+        # ops per call: 2 forms x (iters / 4 + 1 + iters) iterations x 64 MFMAs x 2 * 32^3 ops x 2 * CUs * 4 waves
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        mops = 2 * (iters // 4 + 1 + iters) * 64 * 2.0 * 32 ** 3 * 2 * cus * 4
+        run("mfma", lambda: G.mfma_ceiling(iters), {"int8_ops": mops, "note": "two launches of each MFMA form per call"})
+        run("hbm_read", lambda: big.sum(), {"bytes": big.numel() * 8})
+        run("mall_read", lambda: mall.sum(), {"bytes": mall.numel() * 8})
     sampler.stop_ev.set()
     sampler.join()
 
@@ -175,7 +194,8 @@ def main():
         for r in rows:
             w.writerow(r)
 
-    summary = {"device": info, "period_s": args.period, "samples": len(rows), "sampler_errors": sampler.errors,
+    summary = {"device": info, "workload": f"cfg{args.cfg}: m={m} n={n} k={k} N={N} {'fast' if fast else 'accurate'}",
+               "period_s": args.period, "samples": len(rows), "sampler_errors": sampler.errors,
                "uj_per_energy_count": uj_per_count, "phases": {}}
     for name, ph in phases.items():
         # samples strictly inside the phase (skip the first 20 %: clocks settle after a load change)
