@@ -96,7 +96,8 @@ template <typename R> __device__ __forceinline__ R add_ru(R a, R b);
 template <> __device__ __forceinline__ double add_ru<double>(double a, double b) { return __dadd_ru(a, b); }
 template <> __device__ __forceinline__ float add_ru<float>(float a, float b) { return __fadd_ru(a, b); }
 
-// loads in flight per thread in the stats passes (probe builds vary them: tools/probes/stats_probe.hip)
+// loads in flight per thread in the stats passes (probe builds vary them: tools/probes/stats_probe.hip, in git
+// history at ae0caaa)
 #ifndef OZ2_STRIDED_LOADS
 #define OZ2_STRIDED_LOADS 16
 #endif
@@ -275,7 +276,8 @@ __global__ __launch_bounds__(VT) void stats_contig_kernel(const R *__restrict__ 
 // consecutive VT-chunks are issued before any of them is accumulated; each chain still
 // consumes its elements in increasing order, so the round-up sums are unchanged.
 // ROWS = 16 for m >= 4096; 8 / 4 below, where m/16 blocks leave CUs idle (1024: 15.2 -> 9.6 us,
-// 2048: 23.2 -> 17.3 us; narrower rows cost HBM efficiency at 4096 and up, tools/probes/run_stats_rows.sh).
+// 2048: 23.2 -> 17.3 us; narrower rows cost HBM efficiency at 4096 and up: tools/probes/run_stats_rows.sh,
+// in git history at ae0caaa).
 // ------------------------------------------------------------------
 template <typename R, int VT, int ROWS> struct StridedShared {
     R part[ROWS][VT + 1];
@@ -892,8 +894,11 @@ __global__ __launch_bounds__(256) void mag_vexp_kernel(size_t nvec, size_t ktile
     }
 }
 
-// one wave per (32 vectors, k-tile): lane (r, h) handles vector v0 + r and the 16-byte chunk h of each
-// 32-element half of the tile, so a wave's chunk accesses are 1 KiB contiguous in the panel layout
+// one wave per (32 vectors, FIX_T consecutive k-tiles): lane (r, h) handles vector v0 + r and the 16-byte chunk h
+// of each 32-element half of a tile, so a wave's chunk accesses are 1 KiB contiguous in the panel layout.  The
+// bytes of all FIX_T tiles are loaded before any is rewritten (one wave-tile alone left too few bytes in flight:
+// 3.7-3.9 TB/s, profiles/r05/cfg4_single_stream/)
+constexpr int FIX_T = 4;
 template <typename R, bool CONTIG>
 __global__ __launch_bounds__(256) void mag_fixup_kernel(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
                                                          int8_t *__restrict__ out, size_t ksteps, size_t ktiles,
@@ -901,49 +906,61 @@ __global__ __launch_bounds__(256) void mag_fixup_kernel(const R *__restrict__ X,
                                                          const int *__restrict__ vexp) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
     const size_t v = (size_t)blockIdx.x * 32 + r;
-    const size_t t = (size_t)blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (v >= nvec || t >= ktiles) return;  // padding vectors: pass 1 wrote their zeros
-    uint4 *p0 = reinterpret_cast<uint4 *>(out + panel_offset(v, t * 64 + h * 16, ksteps));
-    uint4 *p1 = reinterpret_cast<uint4 *>(out + panel_offset(v, t * 64 + 32 + h * 16, ksteps));
+    const size_t t0 = ((size_t)blockIdx.y * 4 + (threadIdx.x >> 6)) * FIX_T;
+    if (v >= nvec || t0 >= ktiles) return;  // padding vectors: pass 1 wrote their zeros
+    const int ev = vexp[v];
+    uint4 *p0[FIX_T], *p1[FIX_T];
+    uint4 b0[FIX_T], b1[FIX_T];
+    int2 ti[FIX_T];
     // the bytes are loaded before they are known to be needed: one memory round trip instead of two (the
     // test on b0.x & b1.x, never all ones as every byte is <= 64, keeps the compiler from sinking the loads
     // below the branches)
-    const uint4 b0 = *p0, b1 = *p1;
-    const int ev = vexp[v];
-    const int2 ti = tinfo[t * tstride + v];
-    const bool final_bytes = (ti.x == ev && ti.y != TI_NAN)          // d = 0 (the vector's own amax tile)
-                             || (ti.x == TI_ZERO && ti.y == TI_NONE);  // zeros only
-    if (final_bytes && (b0.x & b1.x) != ~0u) return;
+#pragma unroll
+    for (int i = 0; i < FIX_T; ++i) {
+        const size_t t = t0 + i < ktiles ? t0 + i : t0;  // (a tile past the end repeats t0: loaded, never written)
+        p0[i] = reinterpret_cast<uint4 *>(out + panel_offset(v, t * 64 + h * 16, ksteps));
+        p1[i] = reinterpret_cast<uint4 *>(out + panel_offset(v, t * 64 + 32 + h * 16, ksteps));
+        b0[i] = *p0[i];
+        b1[i] = *p1[i];
+        ti[i] = tinfo[t * tstride + v];
+    }
     const int srow = sft0_scale<R>(sft0_of_exp<R>(ev));  // (as mag_vexp_kernel stored it: no third load)
     constexpr long long EMIN = std::is_same<R, double>::value ? -1022 : -126;
-    const bool exact = ti.y != TI_NAN && ev != INT_MAX && (ti.y == TI_NONE || (long long)ti.y + srow >= EMIN);
-    if (exact) {
-        const int d = min(ev - ti.x, 7);  // (m_t <= 64: from d = 7 on every nonzero byte becomes 1)
-        const uint32_t add = ((1u << d) - 1u) * 0x01010101u, mask = (0xffu >> d) * 0x01010101u;
-        // bytes <= 64: the byte-wise add cannot carry
-        *p0 = make_uint4(((b0.x + add) >> d) & mask, ((b0.y + add) >> d) & mask, ((b0.z + add) >> d) & mask,
-                         ((b0.w + add) >> d) & mask);
-        *p1 = make_uint4(((b1.x + add) >> d) & mask, ((b1.y + add) >> d) & mask, ((b1.z + add) >> d) & mask,
-                         ((b1.w + add) >> d) & mask);
-        return;
-    }
-    // the reference's own arithmetic with the final shift (encode_vec16, MODE 1)
-    for (int half = 0; half < 2; ++half) {
-        const size_t kk = t * 64 + half * 32 + h * 16;
-        uint32_t w[4];
 #pragma unroll
-        for (int dd = 0; dd < 4; ++dd) {
-            uint32_t a = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const size_t e = kk + 4 * dd + b;
-                R re = 0, im;
-                if (e < len) load_elem<R, false, false>(X, CONTIG ? v * ld + e : e * ld + v, re, im);
-                a |= ((uint32_t)mag_byte<R>(scalbn(fabs(re), srow)) & 0xffu) << (8 * b);
-            }
-            w[dd] = a;
+    for (int i = 0; i < FIX_T; ++i) {
+        if (t0 + i >= ktiles) break;
+        const bool final_bytes = (ti[i].x == ev && ti[i].y != TI_NAN)          // d = 0 (the vector's own amax tile)
+                                 || (ti[i].x == TI_ZERO && ti[i].y == TI_NONE);  // zeros only
+        if (final_bytes && (b0[i].x & b1[i].x) != ~0u) continue;
+        const bool exact = ti[i].y != TI_NAN && ev != INT_MAX && (ti[i].y == TI_NONE || (long long)ti[i].y + srow >= EMIN);
+        if (exact) {
+            const int d = min(ev - ti[i].x, 7);  // (m_t <= 64: from d = 7 on every nonzero byte becomes 1)
+            const uint32_t add = ((1u << d) - 1u) * 0x01010101u, mask = (0xffu >> d) * 0x01010101u;
+            // bytes <= 64: the byte-wise add cannot carry
+            *p0[i] = make_uint4(((b0[i].x + add) >> d) & mask, ((b0[i].y + add) >> d) & mask,
+                                ((b0[i].z + add) >> d) & mask, ((b0[i].w + add) >> d) & mask);
+            *p1[i] = make_uint4(((b1[i].x + add) >> d) & mask, ((b1[i].y + add) >> d) & mask,
+                                ((b1[i].z + add) >> d) & mask, ((b1[i].w + add) >> d) & mask);
+            continue;
         }
-        *(half ? p1 : p0) = make_uint4(w[0], w[1], w[2], w[3]);
+        // the reference's own arithmetic with the final shift (encode_vec16, MODE 1)
+        for (int half = 0; half < 2; ++half) {
+            const size_t kk = (t0 + i) * 64 + half * 32 + h * 16;
+            uint32_t w[4];
+#pragma unroll
+            for (int dd = 0; dd < 4; ++dd) {
+                uint32_t a = 0;
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    const size_t e = kk + 4 * dd + b;
+                    R re = 0, im;
+                    if (e < len) load_elem<R, false, false>(X, CONTIG ? v * ld + e : e * ld + v, re, im);
+                    a |= ((uint32_t)mag_byte<R>(scalbn(fabs(re), srow)) & 0xffu) << (8 * b);
+                }
+                w[dd] = a;
+            }
+            *(half ? p1[i] : p0[i]) = make_uint4(w[0], w[1], w[2], w[3]);
+        }
     }
 }
 
@@ -1113,7 +1130,8 @@ bool split_magnitudes(const OperandDesc &d, bool is_A, size_t nvec, size_t len, 
     int *vexp = reinterpret_cast<int *>(ti + ktiles * vpad);
     const int flags = d.contig ? ENC_KFIRST : 0;
     const dim3 g1 = d.contig ? dim3((unsigned)ktiles, (unsigned)(vpad / 64)) : dim3((unsigned)(vpad / 64), (unsigned)ktiles);
-    const dim3 g2((unsigned)((nvec + 63) / 64)), g3((unsigned)((nvec + 31) / 32), (unsigned)((ktiles + 3) / 4));
+    const dim3 g2((unsigned)((nvec + 63) / 64)),
+        g3((unsigned)((nvec + 31) / 32), (unsigned)((ktiles + 4 * FIX_T - 1) / (4 * FIX_T)));
     if (g3.y > 65535) return false;
     const bool nt = nvec * len * (d.dbl ? 8 : 4) >= NT_OPERAND_BYTES;
 #define OZ2_MG(R, C) do { \

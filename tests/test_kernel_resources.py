@@ -17,8 +17,8 @@ pytestmark = pytest.mark.skipif(not shutil.which("llvm-readelf", path="/opt/rocm
 
 # demangled-name prefix -> minimum waves per SIMD
 FLOORS = {
-    "oz2::gemm_i8_persistent_kernel<false, 1, 0>": 2,  # cfg2/3/4 products: 512 threads, 160 KiB LDS, 1 block per CU
-    "oz2::gemm_i8_persistent_kernel<true, 1, 0>": 2,   # cfg5 (Karatsuba sub-products)
+    "oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>": 2,  # cfg2/3/4 products: 512 threads, 160 KiB LDS, 1 block per CU
+    "oz2::gemm_i8_persistent_kernel<true, 1, 0, 0>": 2,  # cfg5 (Karatsuba sub-products)
     "oz2::crt_kernel<0, false, 14u, false, 8>": 5,     # cfg2/3 CRT
     "oz2::crt_kernel<0, false, 10u, false, 8>": 5,     # cfg4 CRT
     "oz2::crt_kernel<2, false, 12u, true, 8>": 3,      # cfg5 CRT (Karatsuba residues)
