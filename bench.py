@@ -69,6 +69,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--no-dgemm", action="store_true")
+    ap.add_argument("--no-cfg3-1gpu", action="store_true", help="N = 1: skip timing cfg3's shape on the one GPU")
     ap.add_argument("--no-variants", action="store_true", help="sharded runs: skip timing the other partitions")
     ap.add_argument("--cpu-sample", type=int, default=0, help="CPU baseline size (default: auto)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -682,6 +683,28 @@ def main():
             dg = 2.0 * m * n * k * reps / (time.perf_counter() - t1) / 1e12
             put(extra, "rocblas_dgemm_tflops_1gpu", round(dg, 2))
             put(extra, "vs_rocblas_dgemm_1gpu", round(value / dg, 3))
+        if world == 1 and wl_name == "cfg2" and not custom and not args.no_cfg3_1gpu:
+            # the multi-GPU lines measure cfg3 (16384^3): its one-GPU time here, so that a 1 -> N curve assembled
+            # from N = 1 (cfg2) and N > 1 (cfg3) lines can also be read against the same workload
+            n3 = WORKLOADS["cfg3"]["size"]
+            A3 = G.randmat(n3, n3, torch.float64, 0.5, 123456, dev)
+            C3 = torch.empty((n3, n3), dtype=torch.float64, device=dev)
+            w3 = G.alloc_work(n3, n3, n3, 14, G.REAL_DEFAULT, dev)
+            one3 = lambda: G.gemm(G.OP_N, G.OP_N, n3, n3, n3, 1.0, A3, n3, A3, n3, 0.0, C3, n3, 14, True, w3)
+            one3()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(3):
+                one3()
+            e1.record()
+            torch.cuda.synchronize()
+            ms3 = e0.elapsed_time(e1) / 3
+            put(extra, "cfg3_workload_1gpu", {"workload": WORKLOADS["cfg3"]["text"].split(",")[0] + " on ONE GPU",
+                                              "ms_per_step": round(ms3, 3),
+                                              "tflops": round(2.0 * n3 ** 3 / (ms3 * 1e-3) / 1e12, 2)})
+            del A3, C3, w3
+            torch.cuda.empty_cache()
         gpu_C = C if (world == 1 and kind == "d" and fast and N == 14) else None
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args.cpu_sample, dev, gpu_C, args.cpu_threads)
         put(report, "cpu", cpu)
