@@ -418,6 +418,58 @@ def test_dist_three_ranks_on_one_gpu_gloo():
     assert "RESULT OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
 
 
+_GRID_CHILD = r'''
+import os, sys
+import torch
+import torch.distributed as dist
+sys.path[:0] = [sys.argv[1], sys.argv[2]]
+from gemmul8 import dist as GD
+from gemmul8 import OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE
+from test_gpu_phases import _rand, _single, _same
+rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+torch.cuda.set_device(0)  # the ranks share the one GPU; gloo carries the messages
+dist.init_process_group("gloo")
+try:
+    m, n, k, N = 900, 1100, 400, 14
+    ok = True
+    for dt in (torch.float64, torch.complex128):
+        ct = COMPLEX_BIG_MATRIX_ENCODE if dt.is_complex else REAL_DEFAULT
+        A, B = _rand(m, k, 11, dt), _rand(k, n, 12, dt)
+        ref = _single(A, B, N, True, dt)
+        # row-major operands: op T on both (A an (m, k) tensor, B an (k, n) one), C (n, m) column-major
+        C = GD.gemm_moduli_grid(OP_T, OP_T, m, n, k, A, k, B, n, N, True, dt, ct, row_blocks=2, gather=True)
+        if rank == 0:
+            ok &= _same(C.t(), ref)
+        Cb = GD.gemm_moduli_grid(OP_T, OP_T, m, n, k, A, k, B, n, N, True, dt, ct, row_blocks=2)
+        G_ = world // 2
+        r0, r1 = GD.blocks(m, 2)[rank // G_]
+        c0, c1 = GD.ShardPlan(r1 - r0, n, N, G_).cols[rank % G_]
+        ok &= _same(Cb.t(), ref[r0:r1, c0:c1])
+    dist.barrier()
+    if rank == 0:
+        print("RESULT", "OK" if ok else "MISMATCH")
+finally:
+    dist.destroy_process_group()
+'''
+
+
+def test_dist_grid_four_ranks_on_one_gpu_gloo():
+    """gemmul8.dist.gemm_moduli_grid with four processes on the one GPU (gloo): two row blocks of two ranks, each a
+    (modulus, column block) partition over its own sub-group, real and complex, gathered and distributed, on the
+    native kernels -- bit-identical to the single call"""
+    import subprocess
+    import sys
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "--no-python", sys.executable, "-c",
+           _GRID_CHILD, tdir, os.path.join(root, "mixed-gemmul8_amd")]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "RESULT OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+
+
 def test_cfg3_size_moduli_shards_simulated_8_ranks():
     """BASELINE cfg3 at full size (16384^3, 14 moduli, fast mode, the reference driver's inputs) through the
     8-rank (modulus, column block) data flow, each simulated rank with its own workspace (8 x 11.5 GiB): the

@@ -8,7 +8,10 @@ part of its receives does not overlap (the last stage's); the collectives (one a
 are left out.
 
     python tools/probes/shard_time.py [size] [N] [W ...]     (defaults: 16384 14 2 4 8)
-    SHARD_ORDER=columns: ShardPlan's column-block-major unit order (default moduli)"""
+    SHARD_ORDER=columns: ShardPlan's column-block-major unit order (default moduli)
+    SHARD_GRID=2: the 2-D grid of gemmul8.dist.gemm_moduli_grid instead -- H = 2 row blocks of W / 2 ranks, each
+    rank replayed as rank (W/2-rank plan) of row block 0's sub-problem (rows [0, m/2) of A; both blocks cost the
+    same)"""
 import os
 import json
 import sys
@@ -56,29 +59,43 @@ def main():
             best = t if best is None else min(best, t)
         return best
 
+    H = int(os.environ.get("SHARD_GRID", "1"))
+    sub_st = {}
     for W in Ws:
-        plan = GD.ShardPlan(m, n, N, W, order=os.environ.get("SHARD_ORDER", "moduli"))
+        Wp, mp, stp = W, m, st
+        if H > 1:  # the grid: row block 0's sub-problem over W / H ranks
+            Wp, mp = W // H, GD.blocks(m, H)[0][1]
+            if mp not in sub_st:
+                ops_h = GD.HipShardOps()
+                sub_st[mp] = ops_h.prepare(G.OP_N, G.OP_N, mp, n, k, A[:, :mp], m, B, k, N, True, torch.float64,
+                                           G.REAL_DEFAULT)
+                Ch = torch.empty((n, mp), dtype=torch.float64, device="cuda")
+                G.gemm(G.OP_N, G.OP_N, mp, n, k, 1.0, A[:, :mp], m, B, k, 0.0, Ch, mp, N, True, sub_st[mp]["work"])
+            stp = sub_st[mp]
+        plan = GD.ShardPlan(mp, n, N, Wp, order=os.environ.get("SHARD_ORDER", "moduli"))
+        st_w = stp
         ranks = []
-        for r in range(W):
+        for r in range(Wp):
+            st = st_w
             j0, j1 = plan.mods[r]
             c0, c1 = plan.cols[r]
             ph = {"stats": timed(lambda: ops.stats(st, plan.rows[r], plan.cols[r])),
                   "encode": timed(lambda: ops.encode(st, j0, j1)) if j1 > j0 else 0.0,
                   "products": [timed(lambda u=u: ops.products(st, *u)) for u in plan.launches[r]],
                   "crt": timed(lambda: ops.recombine(st, c0, c1))}
-            recv = sum((b - a) * m * (3 if st["L"]["nsub"] == 3 else 1)
+            recv = sum((b - a) * mp * (3 if st["L"]["nsub"] == 3 else 1)
                        for t in range(plan.stages) for (_, j, a, b) in plan.recvs(r, t))
             links = {}
             for t in range(plan.stages):
                 for (src, j, a, b) in plan.recvs(r, t):
-                    links[src] = links.get(src, 0) + (b - a) * m
+                    links[src] = links.get(src, 0) + (b - a) * mp
             last = plan.recvs(r, plan.stages - 1) if plan.stages else []
             total = ph["stats"] + ph["encode"] + sum(ph["products"]) + ph["crt"]
             ranks.append({"rank": r, "ms": {kk: (round(v, 3) if not isinstance(v, list) else [round(x, 3) for x in v])
                                             for kk, v in ph.items()},
                           "compute_ms": round(total, 3), "recv_bytes": recv,
                           "max_link_bytes": max(links.values()) if links else 0,
-                          "last_stage_recv_bytes": sum((b - a) * m for (_, j, a, b) in last)})
+                          "last_stage_recv_bytes": sum((b - a) * mp for (_, j, a, b) in last)})
         worst = max(x["compute_ms"] for x in ranks)
         eff = single / (W * worst)
         out["W"][W] = {"ranks": ranks, "slowest_rank_compute_ms": worst,
@@ -89,7 +106,8 @@ def main():
               f"last-stage receive {max(x['last_stage_recv_bytes'] for x in ranks) / 1e6:.0f} MB", flush=True)
         for x in ranks:
             print("   ", json.dumps(x), flush=True)
-    with open("gpurun_out/shard_time_%s.json" % os.environ.get("SHARD_ORDER", "moduli"), "w") as f:
+    with open("gpurun_out/shard_time_%s%s.json" % (os.environ.get("SHARD_ORDER", "moduli"),
+                                                  "_grid%d" % H if H > 1 else ""), "w") as f:
         json.dump(out, f, indent=1)
 
 
