@@ -231,6 +231,19 @@ def cpu_baseline(size_hint, dev, gpu_C=None, threads_req=0):
     if gpu_C is not None and tuple(gpu_C.shape) == (n, n):
         out["bit_identical_to_gpu_C"] = bool(torch.equal(gpu_C.view(torch.uint8), dC.view(torch.uint8)))
     del C1, C2, dA, dC
+    # how the port scales with threads (a 2048^3 sample of the same workload at 1, 2, 4, ... threads up to the
+    # count above), so the rate on a host's every core can be read off without running there
+    A2 = G.randmat(2048, 2048, torch.float64, 0.5, 123456, dev).cpu().numpy().T
+    scaling = {}
+    t = 1
+    while t <= threads:
+        O.set_num_threads(t)
+        t0 = time.perf_counter()
+        O.gemm(A2, A2, 14, True)
+        scaling[str(t)] = round(2.0 * 2048 ** 3 / (time.perf_counter() - t0) / 1e12, 5)
+        t = t * 2 if t * 2 <= threads or t == threads else threads
+    O.set_num_threads(threads)
+    out["thread_scaling_2048_tflops"] = scaling
     # cfg1 in full: SGEMM emulation 1024^3, N = 4, fast mode (BASELINE.json configs[0])
     A1 = G.randmat(1024, 1024, torch.float32, 0.5, 123456, dev).cpu().numpy().T
     t0 = time.perf_counter()
