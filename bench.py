@@ -189,6 +189,20 @@ def _cpu_model():
     return "unknown CPU"
 
 
+def _physical_cores():
+    """distinct (socket, core) pairs in /proc/cpuinfo (the whole host), or None"""
+    try:
+        cores, phys = set(), None
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("physical id"):
+                phys = line.split(":", 1)[1].strip()
+            elif line.startswith("core id"):
+                cores.add((phys, line.split(":", 1)[1].strip()))
+        return len(cores) or None
+    except OSError:
+        return None
+
+
 def cpu_baseline(size_hint, dev, gpu_C=None, threads_req=0):
     """The oracle (CPU restatement, OpenMP) timed on a bounded sample of the cfg2 workload (same generator,
     fast mode, N = 14) and cfg1 (SGEMM emulation 1024^3, N = 4, fast) in full, both on this host.
@@ -244,6 +258,14 @@ def cpu_baseline(size_hint, dev, gpu_C=None, threads_req=0):
         t = t * 2 if t * 2 <= threads or t == threads else threads
     O.set_num_threads(threads)
     out["thread_scaling_2048_tflops"] = scaling
+    # not measured: the value above scaled linearly from its thread count to every physical core of the host (an
+    # upper bound for the port there; the sample above shows how far below linear it scales up to 16 threads)
+    phys = _physical_cores()
+    if phys:
+        out["physical_cores_machine"] = phys
+        out["all_physical_cores_linear_bound"] = {
+            "value": round(out["value"] * phys / threads, 4), "unit": "TFLOP/s", "cores": phys,
+            "basis": f"extrapolated, not measured: value x {phys} / {threads} threads"}
     # cfg1 in full: SGEMM emulation 1024^3, N = 4, fast mode (BASELINE.json configs[0])
     A1 = G.randmat(1024, 1024, torch.float32, 0.5, 123456, dev).cpu().numpy().T
     t0 = time.perf_counter()

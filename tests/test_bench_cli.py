@@ -86,3 +86,14 @@ def test_new_bench_options():
     a = b.parse(["--gpus", "2", "--order", "columns", "--no-single-gpu"])
     assert a.order == "columns" and a.no_single_gpu
     assert b.parse([]).order == "moduli" and not b.parse([]).no_single_gpu
+
+
+def test_physical_core_count_from_cpuinfo(monkeypatch, tmp_path):
+    """cpu_baseline's all-core bound counts distinct (physical id, core id) pairs, not SMT siblings"""
+    b = _bench()
+    text = "".join(f"processor\t: {i}\nphysical id\t: {i // 4 % 2}\ncore id\t\t: {i % 2}\n\n" for i in range(8))
+    f = tmp_path / "cpuinfo"
+    f.write_text(text)
+    real_open = open
+    monkeypatch.setattr("builtins.open", lambda p, *a, **k: real_open(f if p == "/proc/cpuinfo" else p, *a, **k))
+    assert b._physical_cores() == 4  # 2 sockets x 2 cores, each core listed twice
