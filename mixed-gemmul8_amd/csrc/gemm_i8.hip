@@ -49,6 +49,12 @@ constexpr int ACC_I = 4, ACC_J = 2;  // 32 x 32 tiles
 #endif
 
 constexpr int NTHREADS = 512;
+#ifndef OZ2_RES_NTS
+// the persistent kernel's residue stores are non-temporal: they no longer allocate in the L2, where they evicted
+// operand panels (same bits; tools/probes/lib_ab.py, 4 interleaved rounds, profiles/r05/nt_store_ab/: 8192^2 x
+// 1024 -2.4 %, cfg5 -0.3 %, cfg2 -0.2 %).  0 = plain stores (A/B builds)
+#define OZ2_RES_NTS 1
+#endif
 #ifndef OZ2_STAGES
 #define OZ2_STAGES 4
 #endif
@@ -848,8 +854,14 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
             const uint4 v = *reinterpret_cast<const uint4 *>(src + (col & 127) * 64 + ((4 * qd) ^ (x & ~3)));
             const uint32_t e[4] = {v.x, v.y, v.z, v.w};
             const int pm = x & 3;
-            *reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd) =
-                make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+            if (OZ2_RES_NTS) {
+                typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(u4v{e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]},
+                                            reinterpret_cast<u4v *>(out + (size_t)col * g.ldo + 16 * qd));
+            } else {
+                *reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd) =
+                    make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+            }
         }
         __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // park reads done
         barrier();

@@ -36,6 +36,9 @@ __device__ __forceinline__ int center_sum(int a, int b, int p) {
 #ifndef OZ2_ENC_ABLATE
 #define OZ2_ENC_ABLATE 0  // probe builds only (tools/probes/enc_probe.hip, fused_probe.hip)
 #endif
+#ifndef OZ2_ENC_NTS
+#define OZ2_ENC_NTS 0  // probe builds only: 1 = non-temporal slice stores (real operands)
+#endif
 
 // f64 residues in groups of moduli.  mod_8i (scaling.hpp:215-223) reduces the integer-valued x
 // with one f64 step per modulus (x - rint(x/p)*p) and finishes in f32.  Both steps are exact, so
@@ -421,7 +424,11 @@ __device__ __forceinline__ void encode_vec16(const R (&yr)[16], const R (&yi)[16
                 *reinterpret_cast<uint4 *>(o + v * ksteps * KSTEP + kk) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
             else if (OZ2_ENC_ABLATE == 4)  // probe builds only: no slice stores
                 asm volatile("" ::"v"(wr[0]), "v"(wr[1]), "v"(wr[2]), "v"(wr[3]));
-            else
+            else if (OZ2_ENC_NTS) {
+                typedef unsigned u4v __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(u4v{wr[0], wr[1], wr[2], wr[3]},
+                                            reinterpret_cast<u4v *>(o + panel_offset(v, kk, ksteps)));
+            } else
                 *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);
         } else if (kara) {
             *reinterpret_cast<uint4 *>(o + panel_offset(v, kk, ksteps)) = make_uint4(wr[0], wr[1], wr[2], wr[3]);

@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """A/B of whole library builds: python tools/probes/lib_ab.py <variant dir> [<variant dir> ...]
 Each directory holds a gemmul8/ package with its own libgemmul8_amd.so.  Every variant runs in its own
-subprocess, alternating over two rounds: cfg2 (8192^3, N = 14), cfg5 (complex 4096^3, N = 12, Karatsuba
+subprocess, alternating over LIB_AB_ROUNDS (default 2) rounds: cfg2 (8192^3, N = 14), cfg5 (complex 4096^3, N = 12, Karatsuba
 products) and 8192^2 x 1024 (16 k-steps per tile: the epilogue's share is large), 20 timed calls each after
 3 warm-ups; prints ms per call, the phase times (scaling, products, CRT) and a hash of C (the variants must
 agree bit for bit)."""
 import json
+import os
 import subprocess
 import sys
 
@@ -45,7 +46,7 @@ print(json.dumps(out))
 
 def main():
     res = {}
-    for rnd in range(2):
+    for rnd in range(int(os.environ.get("LIB_AB_ROUNDS", "2"))):
         for v in sys.argv[1:]:
             r = subprocess.run([sys.executable, "-c", CHILD, v], capture_output=True, text=True, timeout=300)
             if r.returncode != 0:
