@@ -126,7 +126,11 @@ __device__ __forceinline__ void crt_rows_const(const W (&w)[N], double (&out)[R]
 template <int R> using RowWord = std::conditional_t<R == 8, uint64_t, uint32_t>;
 
 #ifndef OZ2_CRT_NT
-#define OZ2_CRT_NT 0  // probe builds: 1 = non-temporal residue loads, 2 = non-temporal C stores, 3 = both
+// 1 = non-temporal residue loads, 2 = non-temporal C stores, 3 = both (default): the residues are read once and C is
+// not re-read by the next call, so neither needs the caches; the dirty C lines otherwise leave the caches during the
+// next call.  Same bits; tools/probes/lib_ab.py, 4 interleaved rounds, profiles/r05/nt_store_ab/: whole call cfg2
+// -0.2 %, cfg5 -0.6 %, 8192^2 x 1024 -1.1 % against 0 (the CRT phase alone: loads -2.5 %, stores +2-3 %)
+#define OZ2_CRT_NT 3
 #endif
 // residues of rows [off, off+8) of every plane; the fast path is one 8-byte load per plane
 template <unsigned N, typename W = uint64_t>
