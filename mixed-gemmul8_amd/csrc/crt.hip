@@ -136,12 +136,16 @@ template <int R> using RowWord = std::conditional_t<R == 8, uint64_t, uint32_t>;
 template <unsigned N, typename W = uint64_t>
 __device__ __forceinline__ void load_rows(const CrtArgs &a, size_t off, bool fast, int nr, W (&w)[N]) {
     if (fast) {
-        // one per-lane pointer stepped plane by plane (N scalar plane bases would spill the SGPRs)
-        const uint8_t *q = a.R + off;
+        // one per-lane pointer stepped plane by plane (N scalar plane bases would spill the SGPRs); a global
+        // (address space 1) pointer, so the opaque step keeps global_load: a generic one made the compiler emit flat
+        // loads, which also count in lgkmcnt, so every scalar or LDS wait waited for the residues in flight too
+        typedef const __attribute__((address_space(1))) uint8_t *GP;
+        typedef const __attribute__((address_space(1))) W *GW;
+        GP q = (GP)(a.R + off);
 #pragma unroll
         for (unsigned i = 0; i < N; ++i) {
-            if (OZ2_CRT_NT & 1) w[i] = __builtin_nontemporal_load(reinterpret_cast<const W *>(q));
-            else w[i] = *reinterpret_cast<const W *>(q);
+            if (OZ2_CRT_NT & 1) w[i] = __builtin_nontemporal_load((GW)q);
+            else w[i] = *(GW)q;
             q += a.planeR;
             asm volatile("" : "+v"(q));
         }

@@ -61,3 +61,22 @@ def test_hot_kernel_occupancy(table, prefix):
     assert hits, f"{prefix} not in the library"
     for n, v in hits.items():
         assert v["occupancy"] >= FLOORS[prefix], (n, v)
+
+
+@pytest.mark.parametrize("prefix,loads,stores", [
+    ("oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>(", 0, 8),  # residue stores (LDS-DMA loads are buffer ops)
+    ("oz2::gemm_i8_persistent_kernel<true, 1, 0, 0>(", 0, 8),
+    ("oz2::crt_kernel<0, false, 14u, false, 8>(", 14, 4),     # 14 residue planes, C stored in 16-byte vectors
+    ("oz2::crt_kernel<2, false, 12u, true, 8>(", 36, 8),      # 3 Karatsuba sub-planes x 12 moduli
+])
+def test_streaming_memory_ops(prefix, loads, stores):
+    """the streams read or written once per call stay out of the caches (non-temporal), and the
+    CRT's residue loads are global, not flat (a flat load also counts in lgkmcnt, so scalar and LDS waits would
+    wait for the residues in flight)"""
+    import re
+    import kernel_resources as K
+    (body,) = K.disassembly(prefix)
+    ops = [ln.split("//")[0] for ln in body.splitlines() if re.search(r"\s(global|flat)_(load|store)", ln)]
+    assert not [o for o in ops if "flat_load_dwordx2" in o], "residue loads through flat addresses"
+    assert sum("global_load_dwordx2" in o and o.rstrip().endswith(" nt") for o in ops) == loads
+    assert sum("global_store_dwordx4" in o and o.rstrip().endswith(" nt") for o in ops) == stores

@@ -93,6 +93,22 @@ def demangled(names):
     return dict(zip(names, r.stdout.splitlines())) if r.returncode == 0 else {n: n for n in names}
 
 
+def disassembly(prefix, path=LIB):
+    """gfx950 instructions of the kernel(s) whose demangled name starts with `prefix` (one string per kernel)"""
+    out = []
+    for co in _code_objects(_section(path)):
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            txt = subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", "--mcpu=gfx950", "--demangle", f.name],
+                                 check=True, capture_output=True, text=True).stdout
+        for block in txt.split("\n\n"):
+            head = block.lstrip("\n").split("\n", 1)[0]  # "<address> <void name(args)>:"
+            if head.endswith(">:") and (("<" + prefix) in head or ("<void " + prefix) in head):
+                out.append(block)
+    return out
+
+
 def main():
     path = sys.argv[1] if len(sys.argv) > 1 else LIB
     flt = sys.argv[2] if len(sys.argv) > 2 else ""
