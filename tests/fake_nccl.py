@@ -22,7 +22,9 @@ streams, and the GPU tests run the real native steps through it (tests/test_gpu_
   land late.  A consumer that does not wait for them then reads stale columns whenever its stream runs on a
   hardware queue of its own; HIP maps a process's streams onto GPU_MAX_HW_QUEUES (4 here) queues, and two streams
   on one queue run in order, so a missing dependency is caught with high probability, not with certainty;
-- drop_receives=True completes receives without copying (the negative control: results must then differ).
+- drop_receives=True completes receives without copying (the negative control: results must then differ);
+- new_group(ranks): sub-groups as ProcessGroupNCCL has them: their own communicator (P2P channels and collective
+  sequence per group), peers and roots named by global rank, get_rank / get_world_size / get_global_rank per group.
 The host side blocks only to match peers (a send's receiver must have posted before the sender's batch returns,
 a receive's sender before the copy is enqueued), which can only deadlock where the stream-ordered NCCL schedule
 would.  Every tensor a communication stream touches is recorded on it for the caching allocator.
@@ -46,6 +48,11 @@ class _Work:
         return self.ev.query()
 
 
+class _Group:
+    def __init__(self, gid, ranks):
+        self.gid, self.ranks = gid, ranks
+
+
 class FakeNcclWorld:
     def __init__(self, world, timeout_s=120.0, delay_cycles=0, drop_receives=False):
         self.world = world
@@ -55,8 +62,9 @@ class FakeNcclWorld:
         self._cv = threading.Condition()
         self._chan = collections.defaultdict(list)       # (src, dst) -> posted sends, in order
         self._recv_next = collections.defaultdict(int)   # (src, dst) -> index of the next receive
-        self._coll = collections.defaultdict(dict)       # sequence number -> {rank: payload}
-        self._coll_seq = [0] * world
+        self._coll = collections.defaultdict(dict)       # (group id, sequence number) -> {group rank: payload}
+        self._coll_seq = collections.defaultdict(int)    # (group id, rank) -> next sequence number
+        self._groups = {}                                # ranks tuple -> _Group (shared by the rank threads)
         self._tls = threading.local()
         self.calls = collections.Counter()               # what the ranks called (tests assert on it)
         self.module = self._make_module()
@@ -88,16 +96,34 @@ class FakeNcclWorld:
         ev.record(stream)
         return ev
 
-    def _rendezvous(self, payload):
-        """every rank's payload of this collective (the ranks call collectives in the same order)"""
-        r = self.rank
+    # ---- groups ----
+    def new_group(self, ranks=None, **kw):
+        key = tuple(range(self.world)) if ranks is None else tuple(int(r) for r in ranks)
         with self._cv:
-            seq = self._coll_seq[r]
-            self._coll_seq[r] += 1
-            d = self._coll[seq]
+            if key not in self._groups:
+                self._groups[key] = _Group(len(self._groups) + 1, key)
+            return self._groups[key]
+
+    def _members(self, group):
+        return tuple(range(self.world)) if group is None else group.ranks
+
+    def _grank(self, group):
+        m = self._members(group)
+        return m.index(self.rank) if self.rank in m else -1
+
+    def _rendezvous(self, payload, group=None):
+        """every member's payload of this collective, by group rank (the members call the group's collectives in
+        the same order)"""
+        gid, size, r = (0 if group is None else group.gid), len(self._members(group)), self._grank(group)
+        if r < 0:
+            raise RuntimeError(f"fake NCCL: rank {self.rank} is not a member of group {self._members(group)}")
+        with self._cv:
+            seq = self._coll_seq[(gid, r)]
+            self._coll_seq[(gid, r)] += 1
+            d = self._coll[(gid, seq)]
             d[r] = payload
             self._cv.notify_all()
-            self._wait(lambda: len(d) == self.world)
+            self._wait(lambda: len(d) == size)
             return dict(d)
 
     def _finish(self, comm, sync=True):
@@ -118,13 +144,13 @@ class FakeNcclWorld:
                 if op.op is self.module.isend:
                     op.tensor.record_stream(comm)
                     e = {"t": op.tensor, "ready": ready, "done": None}
-                    self._chan[(r, op.peer)].append(e)
+                    self._chan[(0 if op.group is None else op.group.gid, r, op.peer)].append(e)
                     mine.append(e)
             self._cv.notify_all()
         for op in ops:
             if op.op is not self.module.irecv:
                 continue
-            key = (op.peer, r)
+            key = (0 if op.group is None else op.group.gid, op.peer, r)
             with self._cv:
                 idx = self._recv_next[key]
                 self._recv_next[key] += 1
@@ -156,25 +182,25 @@ class FakeNcclWorld:
         self.calls["all_gather"] += 1
         comm = self._start()
         inp.record_stream(comm)
-        d = self._rendezvous((inp, self._event(comm)))
+        d = self._rendezvous((inp, self._event(comm)), group)
         with torch.cuda.stream(comm):
-            for q in range(self.world):
+            for q in range(len(d)):
                 comm.wait_event(d[q][1])
                 outs[q].record_stream(comm)
                 outs[q].copy_(d[q][0])
-        done = self._rendezvous(self._event(comm))
-        for q in range(self.world):
+        done = self._rendezvous(self._event(comm), group)
+        for q in range(len(done)):
             comm.wait_event(done[q])
         self._finish(comm)
 
-    def _combine(self, t, op, root=None):
+    def _combine(self, t, op, root=None, group=None):
         comm = self._start()
         t.record_stream(comm)
-        d = self._rendezvous((t, self._event(comm)))
+        d = self._rendezvous((t, self._event(comm)), group)
         acc = None
-        if root is None or self.rank == root:
+        if root is None or self.rank == root:  # (root: a global rank, as torch.distributed names it)
             with torch.cuda.stream(comm):
-                for q in range(self.world):
+                for q in range(len(d)):
                     comm.wait_event(d[q][1])
                     x = d[q][0]
                     if acc is None:
@@ -183,8 +209,8 @@ class FakeNcclWorld:
                         torch.maximum(acc, x, out=acc)
                     else:
                         acc.add_(x)
-        done = self._rendezvous(self._event(comm))  # every rank has read every input
-        for q in range(self.world):
+        done = self._rendezvous(self._event(comm), group)  # every member has read every input
+        for q in range(len(done)):
             comm.wait_event(done[q])
         if acc is not None:
             with torch.cuda.stream(comm):
@@ -194,16 +220,16 @@ class FakeNcclWorld:
 
     def all_reduce(self, t, op=None, group=None, async_op=False):
         self.calls["all_reduce"] += 1
-        self._combine(t, op or "sum")
+        self._combine(t, op or "sum", group=group)
 
     def reduce(self, t, dst, op=None, group=None, async_op=False):
         self.calls["reduce"] += 1
-        self._combine(t, op or "sum", root=dst)
+        self._combine(t, op or "sum", root=dst, group=group)
 
     def barrier(self, group=None):
         self.calls["barrier"] += 1
         comm = self._start()
-        self._rendezvous(None)
+        self._rendezvous(None, group)
         self._finish(comm)
 
     def _make_module(self):
@@ -220,10 +246,11 @@ class FakeNcclWorld:
             raise NotImplementedError("fake NCCL: use batch_isend_irecv")
 
         return types.SimpleNamespace(
-            get_rank=lambda group=None: world.rank,
-            get_world_size=lambda group=None: world.world,
+            get_rank=lambda group=None: world._grank(group),
+            get_world_size=lambda group=None: len(world._members(group)),
             get_backend=lambda group=None: "nccl",
-            get_global_rank=lambda group, r: r,
+            get_global_rank=lambda group, r: world._members(group)[r],
+            new_group=world.new_group,
             P2POp=P2POp, isend=isend, irecv=irecv,
             ReduceOp=types.SimpleNamespace(SUM="sum", MAX="max"),
             batch_isend_irecv=world.batch_isend_irecv,

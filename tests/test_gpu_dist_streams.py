@@ -145,6 +145,49 @@ def test_planes_to_root_and_partial_sums_reduce(monkeypatch):
     assert world.calls["reduce"] == 2 * W
 
 
+@pytest.mark.parametrize("order", ["moduli", "columns"])
+def test_grid_over_sub_groups(order, monkeypatch):
+    """gemm_moduli_grid under the NCCL branch: 4 ranks in 2 row blocks, each a gemm_moduli over its own sub-group
+    (its own P2P channels and collective sequence), two calls back to back without a host sync: every rank's block
+    and the gathered C (sub-roots to the root over the parent group) equal the single call bit for bit"""
+    import torch
+    import gemmul8 as G
+    from gemmul8 import dist as GD
+    W, H = 4, 2
+    monkeypatch.setattr(GD, "_GRID_GROUPS", {})
+    world = _world(W, monkeypatch)
+    m, n, k, N = 1000, 1536, 1100, 14
+    data = _inputs(m, n, k, (21, 23), torch.float64)
+    refs = [_single(A, B, N, True, torch.float64) for A, B in data]
+
+    def rank(r):
+        ops = GD.HipShardOps()
+
+        def calls():
+            out = []
+            for A, B in data:
+                out.append(GD.gemm_moduli_grid(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, ops=ops, row_blocks=H,
+                                               order=order))
+                out.append(GD.gemm_moduli_grid(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, ops=ops, row_blocks=H,
+                                               gather=True, order=order))
+            return out
+        return _on_own_stream(calls)
+
+    res = run_ranks(world, rank)
+    Gs = W // H
+    for i, ref in enumerate(refs):
+        for r in range(W):
+            h, sub = divmod(r, Gs)
+            r0, r1 = GD.blocks(m, H)[h]
+            c0, c1 = GD.ShardPlan(r1 - r0, n, N, Gs, GD.TILE, order).cols[sub]
+            blk = res[r][2 * i]
+            assert tuple(blk.shape) == (c1 - c0, r1 - r0), (i, r)
+            assert _same(blk.t(), ref[r0:r1, c0:c1]), (i, r)
+        assert _same(res[0][2 * i + 1].t(), ref), i
+        assert all(res[r][2 * i + 1] is None for r in range(1, W))
+    assert len(world._groups) == H  # the sub-groups were created once, not per call
+
+
 def test_negative_control_dropped_transfers(monkeypatch):
     """the comparison depends on the exchanged data: with every receive completed without its copy, the owners'
     blocks differ from the single call (operands no other test uses, so a recycled workspace cannot already hold
