@@ -65,6 +65,7 @@ import os
 import sys
 import threading
 import time
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -676,16 +677,18 @@ def grid_groups(world, row_blocks, group=None):
     """The sub-groups of gemm_moduli_grid: row block h owns the ranks [h G, (h + 1) G) of `group`, G = W / H.
     Created once per (group, W, H); dist.new_group is collective, so every rank of `group` creates all of them,
     in the same order."""
-    # keyed by the parent group object itself (the default group: the current WORLD, so a re-initialised process
-    # group gets new sub-groups; the entry holds the object, so its id cannot be reused by another)
+    # checked against the parent group object itself (the default group: the current WORLD, so a re-initialised
+    # process group gets new sub-groups), held by a weak reference: a process group kept alive past
+    # destroy_process_group is torn down at interpreter exit, where gloo's threads abort the process
     base = group if group is not None else getattr(getattr(dist, "group", None), "WORLD", None)
-    key = (id(group), world, row_blocks)
+    key = (id(base), world, row_blocks)
     hit = _GRID_GROUPS.get(key)
-    if hit is None or hit[0] is not base or hit[1] is not group:
+    if hit is None or hit[0]() is not base:
         G = world // row_blocks
         ranks = [_global(group, r) for r in range(world)]
-        hit = _GRID_GROUPS[key] = (base, group, [dist.new_group(ranks[h * G:(h + 1) * G]) for h in range(row_blocks)])
-    return hit[2]
+        ref = weakref.ref(base) if base is not None else (lambda: None)
+        hit = _GRID_GROUPS[key] = (ref, [dist.new_group(ranks[h * G:(h + 1) * G]) for h in range(row_blocks)])
+    return hit[1]
 
 
 def gemm_moduli_grid(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
