@@ -760,6 +760,7 @@ def main():
         arm("teardown", lambda msg: None)  # the line is out (rank 0) or not this rank's to print
         try:
             dist.barrier()
+            GD.release_grid_groups()
             dist.destroy_process_group()
         except Exception as e:  # a peer that left after a stuck optional phase: the line stands
             print(f"bench: teardown: {type(e).__name__}: {str(e)[:200]}", file=sys.stderr, flush=True)

@@ -76,7 +76,7 @@ from . import (OP_N, OP_T, REAL_DEFAULT, COMPLEX_BIG_MATRIX_ENCODE, alloc_work, 
 __all__ = ["OP_N", "OP_T", "REAL_DEFAULT", "COMPLEX_BIG_MATRIX_ENCODE", "ShardPlan", "HipShardOps", "HipOps", "blocks",
            "moduli_partition", "row_partition", "gemm_moduli", "gemm_moduli_planes_to_root", "matmul_moduli",
            "matmul_rows", "release_workspaces", "side_stream_enabled", "StageWatchdog", "progress",
-           "gemm_moduli_reduce", "gemm_moduli_grid", "grid_groups"]
+           "gemm_moduli_reduce", "gemm_moduli_grid", "grid_groups", "release_grid_groups"]
 
 TILE = 256  # product tile edge: column blocks of the product units start at multiples of it
 WORKSPACE_CACHE = 2  # workspaces (shapes) kept per native ops object
@@ -689,6 +689,12 @@ def grid_groups(world, row_blocks, group=None):
         ref = weakref.ref(base) if base is not None else (lambda: None)
         hit = _GRID_GROUPS[key] = (ref, [dist.new_group(ranks[h * G:(h + 1) * G]) for h in range(row_blocks)])
     return hit[1]
+
+
+def release_grid_groups():
+    """Drop the cached sub-groups of gemm_moduli_grid (call before destroy_process_group: the handles are useless
+    afterwards and need not outlive it)."""
+    _GRID_GROUPS.clear()
 
 
 def gemm_moduli_grid(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
