@@ -697,6 +697,9 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
     const size_t e0 = (size_t)(kfirst ? bx : by) * KT;
     const int tid = threadIdx.x;
 
+    // this thread's vector's shift, loaded with the tile (after the barrier it cost one more memory round trip)
+    const size_t vs = v0 + (tid & 63);
+    const int16_t sraw = vs < nvec ? sft[vs] : int16_t(0);
     // stage the tile, coalesced along whichever index is contiguous in HBM; interior tiles
     // load without per-element guards so all loads are in flight at once
     constexpr int NL = (64 * KT) / NT;
@@ -743,7 +746,7 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
     const size_t v = v0 + vl;
     const size_t kk = e0 + 16 * c;
     int s = 0;
-    if (v < nvec) s = MODE != 1 ? -(int)sft[v] : sft0_scale<R>(sft[v]);
+    if (v < nvec) s = MODE != 1 ? -(int)sraw : sft0_scale<R>(sraw);
 
     R yr[16], yi[16];
 #pragma unroll
