@@ -520,7 +520,8 @@ def main():
     # the K steps are timed with HIP events on the stream, recorded inside the barrier +
     # synchronize bracket: the GPU timeline of the steps, idle time between calls included.  The host wall time of
     # the bracket is reported beside it (ms_per_step_wall); it also holds the host's return from the closing
-    # synchronize (profiles/r04/final4: wall steps 0.01-0.5 ms above the summed kernel phases, tools/probes/gap_probe.py)
+    # synchronize (profiles/r04/final4: wall steps 0.01-0.5 ms above the summed kernel phases; tools/probes/gap_probe.py,
+    # in git history at ae0caaa)
     e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e_start.record()
