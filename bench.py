@@ -70,6 +70,7 @@ def parse(argv=None):
     ap.add_argument("--no-accuracy", action="store_true")
     ap.add_argument("--no-dgemm", action="store_true")
     ap.add_argument("--no-cfg3-1gpu", action="store_true", help="N = 1: skip timing cfg3's shape on the one GPU")
+    ap.add_argument("--no-power", action="store_true", help="no amdsmi power / clock sampling during the timed steps")
     ap.add_argument("--no-variants", action="store_true", help="sharded runs: skip timing the other partitions")
     ap.add_argument("--cpu-sample", type=int, default=0, help="CPU baseline size (default: auto)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -160,6 +161,66 @@ def dist_setup():
     else:
         torch.cuda.set_device(0)
     return world, rank, backend
+
+
+class StepPower:
+    """Board power and clocks of this process's GPU while a loop of steps runs (sampled in
+    process): the SMU's gpu_metrics table read through amdsmi every `period` s by a thread (tools/power_trace.py's
+    sampler), and the energy accumulator across the loop.  Any failure (no amdsmi, no permission) leaves the line
+    without the field."""
+
+    def __init__(self, period=0.005):
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import amdsmi
+        import power_trace as PT
+        amdsmi.amdsmi_init()
+        self.smi, self.PT, self.period = amdsmi, PT, period
+        self.dev, _ = PT.find_device(amdsmi)
+        cap = amdsmi.amdsmi_get_power_cap_info(self.dev)
+        self.cap_w = cap.get("power_cap", 0) / 1e6 if isinstance(cap, dict) else None
+        self.sampler, self.e0 = None, None
+
+    def _energy(self):
+        e = self.smi.amdsmi_get_energy_count(self.dev)
+        self.res = float(e.get("counter_resolution") or 15.259)  # microjoules per count
+        return e["energy_accumulator"] * self.res * 1e-6, time.perf_counter()
+
+    def begin(self):
+        self.e0 = self._energy()
+        self.sampler = self.PT.Sampler(self.smi, self.dev, self.period)
+        self.sampler.phase = "steps"
+        self.sampler.start()
+
+    def end(self, steps, settle=0.0):
+        e1 = self._energy()
+        self.sampler.stop_ev.set()
+        self.sampler.join()
+        rows = self.sampler.rows[int(len(self.sampler.rows) * settle):]
+        mean = lambda key: round(sum(r[key] for r in rows if r.get(key) is not None) /
+                                 max(1, sum(1 for r in rows if r.get(key) is not None)), 1)
+        clk = [sum(r[f"gfxclk{i}"] for i in range(8)) / 8 for r in rows if all(r.get(f"gfxclk{i}") for i in range(8))]
+        out = {"samples": len(rows), "period_ms": self.period * 1e3, "power_cap_W": self.cap_w,
+               "socket_power_W_mean": mean("current_socket_power"),
+               "gfxclk_MHz_mean_8xcd": round(sum(clk) / len(clk), 1) if clk else None,
+               "hotspot_C_mean": mean("temperature_hotspot")}
+        total = e1[1] - self.e0[1]
+        a, b = (rows[0], rows[-1]) if len(rows) >= 2 else (None, None)
+        if a and a.get("energy_accumulator") is not None and b.get("energy_accumulator") is not None and total > 0:
+            # over the settled window, from the samples' own accumulator readings (the step rate is the loop's)
+            joules, dt = (b["energy_accumulator"] - a["energy_accumulator"]) * self.res * 1e-6, b["t"] - a["t"]
+            if dt > 0 and joules > 0:
+                out["energy_per_step_J"] = round(joules / (steps * dt / total), 4)
+                out["power_from_energy_W"] = round(joules / dt, 1)
+        if a and a.get("ppt_residency_acc") is not None and b.get("accumulation_counter") and \
+                b["accumulation_counter"] > a["accumulation_counter"]:
+            out["ppt_limiter_residency"] = round((b["ppt_residency_acc"] - a["ppt_residency_acc"]) /
+                                                 (b["accumulation_counter"] - a["accumulation_counter"]), 3)
+        out["loop_ms_per_step"] = round(total / steps * 1e3, 4) if steps else None
+        try:
+            self.smi.amdsmi_shut_down()
+        except Exception:
+            pass
+        return out
 
 
 def barrier(world):
@@ -611,6 +672,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": report["cpu"],
         }
+
         if sharded:
             out["config"]["unit_order"] = args.order
             out["config"]["dist_side_stream"] = GD.side_stream_enabled() and backend == "nccl"
@@ -710,6 +772,23 @@ def main():
         if ceiling > 0:
             put(roofline, "data_bound_ceiling", round(ceiling, 1))
             put(roofline, "frac_of_data_bound_ceiling", round(achieved / ceiling, 4))
+        if world == 1 and not args.no_power:
+            # the box's power state on this step, after the timed region: the SMU averages over longer than the
+            # K timed steps, so the same step runs back to back for about a second while amdsmi is sampled every
+            # 5 ms (the first 30 % of the window dropped while the clock settles); the power-capped clock differs
+            # from device to device, and this is what a line from a slow box shows
+            try:
+                sp = StepPower()
+                sp.begin()
+                t_p, calls = time.perf_counter(), 0
+                while time.perf_counter() - t_p < 1.0:
+                    for _ in range(4):
+                        step()
+                    calls += 4
+                    torch.cuda.synchronize()
+                put(extra, "power_steady_state", sp.end(calls, settle=0.3))
+            except Exception as e:  # (fail-soft: the line goes without the field)
+                print(f"bench: no power sample: {type(e).__name__}: {str(e)[:120]}", file=sys.stderr, flush=True)
         if not args.no_dgemm and kind == "d" and (world == 1 or sharded):
             # the vendor DGEMM of the same shape on ONE GPU (rocBLAS through torch)
             Ar, Br = A.t(), B.t()

@@ -97,3 +97,34 @@ def test_physical_core_count_from_cpuinfo(monkeypatch, tmp_path):
     real_open = open
     monkeypatch.setattr("builtins.open", lambda p, *a, **k: real_open(f if p == "/proc/cpuinfo" else p, *a, **k))
     assert b._physical_cores() == 4  # 2 sockets x 2 cores, each core listed twice
+
+
+def test_step_power_sampler_fields(monkeypatch):
+    """bench.StepPower (the N = 1 line's power_steady_state) against a stand-in amdsmi: energy per step from the
+    settled window's accumulator readings, clocks averaged over the 8 XCDs, PPT residency from the accumulators"""
+    import time
+    import types
+    t0 = time.perf_counter()
+    tick = lambda: time.perf_counter() - t0
+    fake = types.SimpleNamespace(
+        amdsmi_init=lambda: None, amdsmi_shut_down=lambda: None,
+        amdsmi_get_power_cap_info=lambda d: {"power_cap": 1400000000},
+        # 1400 W: 1400 J/s = 1400e6 uJ/s at 15.3 uJ per count
+        amdsmi_get_energy_count=lambda d: {"energy_accumulator": int(tick() * 1400e6 / 15.3),
+                                           "counter_resolution": 15.3},
+        amdsmi_get_gpu_metrics_info=lambda d: {
+            "current_socket_power": 1400, "current_gfxclks": [1600] * 8, "temperature_hotspot": 60,
+            "energy_accumulator": int(tick() * 1400e6 / 15.3), "ppt_residency_acc": int(tick() * 1e6),
+            "accumulation_counter": int(tick() * 1e6)})
+    monkeypatch.setitem(sys.modules, "amdsmi", fake)
+    b = _bench()
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import power_trace
+    monkeypatch.setattr(power_trace, "find_device", lambda smi: ("dev", "bdf"))
+    sp = b.StepPower(period=0.002)
+    sp.begin()
+    time.sleep(0.2)
+    out = sp.end(100, settle=0.3)  # 100 steps in 0.2 s: 2 ms and 2.8 J per step at 1400 W
+    assert out["power_cap_W"] == 1400 and out["gfxclk_MHz_mean_8xcd"] == 1600 and out["socket_power_W_mean"] == 1400
+    assert abs(out["power_from_energy_W"] - 1400) < 50 and abs(out["energy_per_step_J"] - 2.8) < 0.2
+    assert out["ppt_limiter_residency"] == 1.0 and out["samples"] > 10 and abs(out["loop_ms_per_step"] - 2.0) < 0.3

@@ -14,11 +14,11 @@ BENCH_ARGS="$@"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-# --no-cfg3-1gpu: the N = 1 line's extra timing of cfg3's 16384^3 shape (after the timed region) would mix a second
-# shape into the per-kernel averages
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py --no-cfg3-1gpu $BENCH_ARGS \
+# --no-cfg3-1gpu, --no-power: the N = 1 line's extra timing of cfg3's 16384^3 shape and its one-second power loop
+# (after the timed region) would mix a second shape and ~160 extra launches into the per-kernel averages
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o run -- python3 bench.py --no-cfg3-1gpu --no-power $BENCH_ARGS \
   > $OUT/bench.json 2> $OUT/trace.log
-PMC_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-accuracy --no-dgemm --no-cfg3-1gpu $BENCH_ARGS"
+PMC_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-accuracy --no-dgemm --no-cfg3-1gpu --no-power $BENCH_ARGS"
 i=0
 for grp in "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" "TCC_HIT_sum TCC_MISS_sum" "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS"; do
   i=$((i+1))
