@@ -147,10 +147,17 @@ def dist_setup():
             # groups on fd 1 (gloo does), and stdout must carry rank 0's one JSON line only
             sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd"))
             from gemmul8 import dist as GD
+            ok = 1
             try:
                 GD.grid_groups(world, 2)
             except Exception as e:  # the variant then reports its failure; the measured line does not depend on it
                 print(f"bench: grid sub-groups: {type(e).__name__}: {str(e)[:200]}", file=sys.stderr, flush=True)
+                ok = 0
+            # every rank skips the variant if any rank failed: a rank entering the sub-group collectives alone
+            # would stall the variant phase until the watchdog (MIN over ranks of a success flag)
+            flag = torch.tensor([ok], dtype=torch.int32, device=f"cuda:{local}" if backend == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if int(flag.item()) == 0:
                 os.environ["GEMMUL8_BENCH_NO_GRID"] = "1"
         dist.barrier()  # the connections are up before stdout is given back
         world = dist.get_world_size()

@@ -234,14 +234,35 @@ def _check_sums(sums, m, n):
         raise ValueError(f"partial CRT sums hold {sums.numel()} doubles, need 2 * n * m = {2 * n * m}")
 
 
-def crt_finish(m, n, k, num_moduli, alpha, beta, C, ldc, work, sums, stream=None):
-    """C = alpha * CRT(summed partials) scaled by the workspace's shifts + beta * C (real outputs)."""
+def _check_colmajor(name, X, rows, cols, ld):
+    """X addresses a column-major rows x cols matrix with leading dimension ld: unit stride within a column,
+    ld between columns (a (cols, rows) view of a (cols, ld) tensor, e.g. a sub-matrix), and the storage behind
+    the view reaches the last element"""
+    if ld < rows:
+        raise ValueError(f"{name}: leading dimension {ld} < {rows} rows")
+    if rows == 0 or cols == 0:
+        return
+    col_stride = X.stride(0) if X.dim() == 2 else ld
+    if X.dim() not in (1, 2) or X.stride(-1) != 1 or (cols > 1 and X.dim() == 2 and X.shape[0] > 1 and col_stride != ld):
+        raise ValueError(f"{name}: shape {tuple(X.shape)} strides {X.stride()} is not a column-major layout with "
+                         f"unit row stride and ld = {ld}")
+    extent = X.storage_offset() + ld * (cols - 1) + rows
+    avail = X.untyped_storage().nbytes() // X.element_size()
+    if extent > avail:
+        raise ValueError(f"{name}: a column-major {rows} x {cols} matrix with ld = {ld} needs {extent} elements of "
+                         f"storage from the view's base, the tensor's storage holds {avail}")
+
+
+def crt_finish(m, n, k, num_moduli, alpha, beta, C, ldc, work, sums, stream=None, out_dtype=None):
+    """C = alpha * CRT(summed partials) scaled by the workspace's shifts + beta * C (real outputs).
+    C: a column-major m x n matrix with leading dimension ldc (any view with unit row stride and column stride
+    ldc, as gemm() accepts).  out_dtype: the output type crt_partial was called with, checked against C's."""
     _check_sums(sums, m, n)
     if C.dtype not in (torch.float64, torch.float32):
         raise TypeError(f"crt_finish: C must be float64 or float32, not {C.dtype}")
-    if ldc < m or not C.is_contiguous() or C.numel() < ldc * (n - 1) + m:
-        raise ValueError(f"crt_finish: C (numel {C.numel()}, contiguous {C.is_contiguous()}) does not hold a "
-                         f"column-major {m} x {n} matrix with ldc = {ldc}")
+    if out_dtype is not None and C.dtype != out_dtype:
+        raise TypeError(f"crt_finish: C is {C.dtype}, the partial sums were formed for {out_dtype}")
+    _check_colmajor("crt_finish: C", C, m, n, ldc)
     al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
     _check(lib.gemmul8_crt_finish(_stream(stream), m, n, k, num_moduli, _DTYPE[C.dtype], REAL_DEFAULT, al.ptr, be.ptr,
                                   C.data_ptr(), ldc, work.data_ptr(), sums.data_ptr(), m))

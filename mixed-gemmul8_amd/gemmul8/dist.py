@@ -378,7 +378,7 @@ class HipShardOps:
         """C (an (n, m) tensor) from the summed partial CRT sums and the workspace's shifts"""
         m, n = st["m"], st["n"]
         C = torch.empty((n, m), dtype=st["dtype"], device=st["dev"])
-        crt_finish(m, n, st["k"], st["N"], 1.0, 0.0, C, m, st["work"], S)
+        crt_finish(m, n, st["k"], st["N"], 1.0, 0.0, C, m, st["work"], S, out_dtype=st["dtype"])
         return C
 
     def side_stream(self):
@@ -675,19 +675,25 @@ _GRID_GROUPS = {}
 
 def grid_groups(world, row_blocks, group=None):
     """The sub-groups of gemm_moduli_grid: row block h owns the ranks [h G, (h + 1) G) of `group`, G = W / H.
-    Created once per (group, W, H); dist.new_group is collective, so every rank of `group` creates all of them,
-    in the same order."""
+    Created once per (group, W, H), by every rank of `group`, all of them in the same order.
+
+    dist.new_group is collective over the default (WORLD) group unless use_local_synchronization=True: with
+    `group` the WORLD group (or None) every process enters it, as required; with a smaller parent group the
+    processes outside it never call here, so the sub-groups are created with local synchronization (only the
+    members of each sub-group synchronise; a rank of `group` outside a sub-group gets the non-member handle)."""
     # checked against the parent group object itself (the default group: the current WORLD, so a re-initialised
     # process group gets new sub-groups), held by a weak reference: a process group kept alive past
     # destroy_process_group is torn down at interpreter exit, where gloo's threads abort the process
-    base = group if group is not None else getattr(getattr(dist, "group", None), "WORLD", None)
+    wgroup = getattr(getattr(dist, "group", None), "WORLD", None)
+    base = group if group is not None else wgroup
     key = (id(base), world, row_blocks)
     hit = _GRID_GROUPS.get(key)
     if hit is None or hit[0]() is not base:
         G = world // row_blocks
         ranks = [_global(group, r) for r in range(world)]
         ref = weakref.ref(base) if base is not None else (lambda: None)
-        hit = _GRID_GROUPS[key] = (ref, [dist.new_group(ranks[h * G:(h + 1) * G]) for h in range(row_blocks)])
+        kw = {} if base is wgroup else {"use_local_synchronization": True}
+        hit = _GRID_GROUPS[key] = (ref, [dist.new_group(ranks[h * G:(h + 1) * G], **kw) for h in range(row_blocks)])
     return hit[1]
 
 

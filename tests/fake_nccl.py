@@ -97,12 +97,22 @@ class FakeNcclWorld:
         return ev
 
     # ---- groups ----
-    def new_group(self, ranks=None, **kw):
+    def new_group(self, ranks=None, use_local_synchronization=False, **kw):
+        """torch.distributed's rule: new_group is collective over the WHOLE world (every process enters it, in
+        the same order) unless use_local_synchronization=True, when only the members synchronise and a
+        non-member returns at once.  A rank that skips a world-collective creation leaves the others waiting
+        (TimeoutError here, a hang under NCCL)."""
         key = tuple(range(self.world)) if ranks is None else tuple(int(r) for r in ranks)
         with self._cv:
             if key not in self._groups:
                 self._groups[key] = _Group(len(self._groups) + 1, key)
-            return self._groups[key]
+            g = self._groups[key]
+        self.calls["new_group"] += 1
+        if not use_local_synchronization:
+            self._rendezvous(("new_group", key))  # the world group's sequence: every rank, same order
+        elif self.rank in key:
+            self._rendezvous(("new_group_local", key), g)
+        return g
 
     def _members(self, group):
         return tuple(range(self.world)) if group is None else group.ranks

@@ -1,4 +1,6 @@
-"""CPU check of the committed 8-rank rehearsal of the driver's multi-GPU bench:
+"""ARTIFACT CHECK (it parses a committed file; it does not run bench.py or gemmul8.dist, so it stays green whatever
+they become -- tests/test_bench_cli.py and tests/test_dist.py test the code).  CPU check of the committed 8-rank
+rehearsal of the driver's multi-GPU bench:
 `GEMMUL8_BENCH_BACKEND=gloo python bench.py --gpus 8 --size 2048` on one GPU (8 ranks sharing the device, so its
 timings mean nothing) must produce ONE complete line: the cfg3-style sharded step, the single-GPU baseline, the
 accuracy check and every partition variant timed, nothing marked incomplete or failed.  The line is the one

@@ -269,6 +269,47 @@ def test_sharded_equals_single_call(tmp_path, world, case):
         assert np.array_equal(got.view(np.uint8), np.ascontiguousarray(C[:, c0:c1]).view(np.uint8)), r
 
 
+def _grid_parent_worker(rank, world, port, outdir):
+    """gemm_moduli_grid over a parent group of ranks 0-3 of a 6-process world: processes 4 and 5
+    never call it, so the row-block sub-groups must be created with local synchronization; op N operands (the
+    path bench.py times: A[:, r0:r1] is a strided view of the (k, m) storage with lda = m)"""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "mixed-gemmul8_amd")]
+    from gemmul8 import dist as GD
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m, n, k, N = 90, 70, 50, 12
+        rng = np.random.default_rng(11)
+        A = (rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))
+        B = (rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))
+        parent = dist.new_group([0, 1, 2, 3])  # world-collective: every process enters
+        if rank < 4:
+            At = torch.from_numpy(np.ascontiguousarray(A.T))  # column-major m x k: the (k, m) tensor
+            Bt = torch.from_numpy(np.ascontiguousarray(B.T))
+            Cg = GD.gemm_moduli_grid(0, 0, m, n, k, At, m, Bt, k, N, True, ops=OracleShardOps(), group=parent,
+                                     row_blocks=2, gather=True, align=16)
+            if rank == 0:
+                np.save(os.path.join(outdir, "grid_parent.npy"), Cg.t().contiguous().numpy())
+            else:
+                assert Cg is None
+            GD.release_grid_groups()
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_grid_over_non_world_parent_group(tmp_path):
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    mp.spawn(_grid_parent_worker, args=(6, _free_port(), str(tmp_path)), nprocs=6, join=True)
+    m, n, k, N = 90, 70, 50, 12
+    rng = np.random.default_rng(11)
+    A = (rng.random((m, k)) - 0.5) * np.exp(rng.standard_normal((m, k)))
+    B = (rng.random((k, n)) - 0.5) * np.exp(rng.standard_normal((k, n)))
+    C = np.ascontiguousarray(O.gemm(A, B, N, True))
+    got = np.load(tmp_path / "grid_parent.npy")
+    assert got.shape == C.shape and np.array_equal(got.view(np.uint8), C.view(np.uint8))
+
+
 def test_partitions():
     sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd"))
     from gemmul8.dist import moduli_partition, row_partition

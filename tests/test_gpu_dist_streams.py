@@ -145,11 +145,13 @@ def test_planes_to_root_and_partial_sums_reduce(monkeypatch):
     assert world.calls["reduce"] == 2 * W
 
 
-@pytest.mark.parametrize("order", ["moduli", "columns"])
-def test_grid_over_sub_groups(order, monkeypatch):
+@pytest.mark.parametrize("order,op", [("moduli", "T"), ("columns", "T"), ("moduli", "N")])
+def test_grid_over_sub_groups(order, op, monkeypatch):
     """gemm_moduli_grid under the NCCL branch: 4 ranks in 2 row blocks, each a gemm_moduli over its own sub-group
     (its own P2P channels and collective sequence), two calls back to back without a host sync: every rank's block
-    and the gathered C (sub-roots to the root over the parent group) equal the single call bit for bit"""
+    and the gathered C (sub-roots to the root over the parent group) equal the single call bit for bit.  op N is
+    the path bench.py times: the row block of op(A) is then a strided column range A[:, r0:r1] of the (k, m)
+    storage, passed with the parent's lda = m"""
     import torch
     import gemmul8 as G
     from gemmul8 import dist as GD
@@ -159,6 +161,10 @@ def test_grid_over_sub_groups(order, monkeypatch):
     m, n, k, N = 1000, 1536, 1100, 14
     data = _inputs(m, n, k, (21, 23), torch.float64)
     refs = [_single(A, B, N, True, torch.float64) for A, B in data]
+    if op == "N":  # column-major m x k / k x n storage of the same matrices
+        data = [(A.t().contiguous(), B.t().contiguous()) for A, B in data]
+        torch.cuda.synchronize()
+    gop, lda, ldb = (G.OP_N, m, k) if op == "N" else (G.OP_T, k, n)
 
     def rank(r):
         ops = GD.HipShardOps()
@@ -166,9 +172,9 @@ def test_grid_over_sub_groups(order, monkeypatch):
         def calls():
             out = []
             for A, B in data:
-                out.append(GD.gemm_moduli_grid(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, ops=ops, row_blocks=H,
+                out.append(GD.gemm_moduli_grid(gop, gop, m, n, k, A, lda, B, ldb, N, True, ops=ops, row_blocks=H,
                                                order=order))
-                out.append(GD.gemm_moduli_grid(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, ops=ops, row_blocks=H,
+                out.append(GD.gemm_moduli_grid(gop, gop, m, n, k, A, lda, B, ldb, N, True, ops=ops, row_blocks=H,
                                                gather=True, order=order))
             return out
         return _on_own_stream(calls)
@@ -186,6 +192,41 @@ def test_grid_over_sub_groups(order, monkeypatch):
         assert _same(res[0][2 * i + 1].t(), ref), i
         assert all(res[r][2 * i + 1] is None for r in range(1, W))
     assert len(world._groups) == H  # the sub-groups were created once, not per call
+
+
+def test_grid_over_non_world_parent(monkeypatch):
+    """gemm_moduli_grid over a parent group smaller than the world: 6 processes, the call runs on
+    the 4 ranks of a sub-group only.  new_group is collective over the WHOLE world unless it synchronises
+    locally (tests/fake_nccl.py enforces it), so the row-block sub-groups must be created with local
+    synchronization, else ranks 0-3 wait for 4 and 5 forever (a hang under RCCL).  Blocks bit-identical to
+    the single call"""
+    import torch
+    import gemmul8 as G
+    from gemmul8 import dist as GD
+    W, H = 6, 2
+    monkeypatch.setattr(GD, "_GRID_GROUPS", {})
+    world = FakeNcclWorld(W, timeout_s=60.0, delay_cycles=DELAY)
+    monkeypatch.setattr(GD, "dist", world.module)
+    m, n, k, N = 700, 900, 650, 12
+    (A, B), = _inputs(m, n, k, (31,), torch.float64)
+    ref = _single(A, B, N, True, torch.float64)
+
+    def rank(r):
+        parent = world.module.new_group([0, 1, 2, 3])  # every process enters (world-collective creation)
+        if r >= 4:
+            return None
+        ops = GD.HipShardOps()
+        return _on_own_stream(lambda: GD.gemm_moduli_grid(G.OP_T, G.OP_T, m, n, k, A, k, B, n, N, True, ops=ops,
+                                                          group=parent, row_blocks=H))
+
+    res = run_ranks(world, rank)
+    Gs = 4 // H
+    for r in range(4):
+        h, sub = divmod(r, Gs)
+        r0, r1 = GD.blocks(m, H)[h]
+        c0, c1 = GD.ShardPlan(r1 - r0, n, N, Gs, GD.TILE, "moduli").cols[sub]
+        assert _same(res[r].t(), ref[r0:r1, c0:c1]), r
+    assert res[4] is None and res[5] is None
 
 
 def test_negative_control_dropped_transfers(monkeypatch):

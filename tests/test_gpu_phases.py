@@ -117,6 +117,19 @@ def test_partial_crt_sums(m, n, k, N, fast, dt):
     G.recombine(m, n, k, N, 2.5, -0.5, Cref, m, work)
     torch.cuda.synchronize()
     assert _same(Cab, Cref)
+    # a column-major sub-matrix view with ldc > m (as gemm() accepts), and the out_dtype check
+    ldc = m + 37
+    big = torch.full((n + 2, ldc), 7.0, dtype=tdt, device="cuda")
+    Cv = big[1:n + 1, :m]
+    G.crt_finish(m, n, k, N, 1.0, 0.0, Cv, ldc, work, full, out_dtype=tdt)
+    torch.cuda.synchronize()
+    assert _same(Cv.t(), ref) and bool((big[0] == 7).all()) and bool((big[n + 1] == 7).all())
+    assert bool((big[1:n + 1, m:] == 7).all())
+    with pytest.raises(TypeError):
+        G.crt_finish(m, n, k, N, 1.0, 0.0, Ct, m, work, full,
+                     out_dtype=torch.float32 if tdt == torch.float64 else torch.float64)
+    with pytest.raises(ValueError):  # the view's storage ends before the last column
+        G.crt_finish(m, n, k, N, 1.0, 0.0, big[3:n + 2, :m], ldc, work, full)
 
 
 @pytest.mark.parametrize("fast", [True, False])
