@@ -26,6 +26,7 @@
 // HBM -> LDS through a 4-slot ring (128 KiB) with LDS-DMA issued three k-steps
 // ahead; waits are counted by hand (vmcnt), barriers are raw s_barrier.
 #include <atomic>
+#include <type_traits>
 
 #include "oz2_split.hpp"
 
@@ -880,6 +881,217 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
 #undef OZ2_STAMP
 }
 
+// ---------------------------------------------------------------------------------------------
+// Persistent residue product with PER-GROUP epilogues (round 6).  The same DMA pipeline, tile queues and
+// main loop as gemm_i8_persistent_kernel, but the two wave groups (rows 0-127 / 128-255 of the tile) stay one
+// barrier apart for the whole launch: no realignment around the epilogue.  Each group parks and stores its
+// own 128 rows right after its own last MFMA interval, so per SIMD the intervals pair as
+//     group 0:  ... M(K-1) | park | store | L'(0) | M'(0) ...
+//     group 1:  ... L(K-1) | M(K-1) | park | store | L'(0) ...
+// (L = fragment reads + DMA issue, M = MFMAs; ' = the next tile): group 0's park runs beside group 1's last
+// MFMAs, and the two epilogues overlap each other instead of following each other with the whole block
+// waiting at four barriers.  Per tile each group passes 2K + 2 barriers.
+// Group 0 parks in the ring slot of the tile's last step (its next writer is group 0's own DMA of the next
+// tile's step 3, issued in L'(0) after its store sweep has read the slot back), group 1 in the spare 32 KiB.
+// The accumulators are not reset: the first MFMA of each tile reads its C operand from a splat of the
+// tile's bias (or 0) and writes the accumulator, i.e. no 128 v_mov per wave and tile.
+// The tile after next is claimed by thread 0 at the start of group 0's park; it is published in the spare's
+// first dword during group 0's MFMA interval of the next tile's step 0 (group 1 has read its parked
+// residues back by then) and read by every wave after step 1, as before.
+// Park layout of a group's 128 x 256 residue block: [256 cols][32 dwords], dword d = 4 consecutive rows
+// 4d..4d+3; the 16-byte chunk c = d >> 2 of column col sits at chunk position c ^ ((col >> 1) & 7) and its
+// dword q at (q ^ 2 (col & 1)): conflict-free ds_write_b32 of a 16 x 16 accumulator tile (32 lanes, 32 banks)
+// and ds_read_b128 of 8 columns x 128 B per wave.
+__device__ __forceinline__ void mfma_step_first(AccTile (&acc)[ACC_I][ACC_J], const Frags &f, const v4i c) {
+#pragma unroll
+    for (int x = 0; x < 32; ++x) {
+        const int i = x >> 2, jj = x & 3;
+        acc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[i], f.b[jj], c, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool SUB, int PRIO = 1>
+__global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(GemmArgs g) {
+    static_assert(OZ2_MFMA16, "per-group epilogue: 16x16x64 accumulator map");
+    __shared__ __attribute__((aligned(1024))) int8_t smem[PLDS_BYTES + PARK_SPARE];
+    static_assert(PLDS_BYTES + PARK_SPARE <= 160 * 1024, "LDS");
+    static_assert(PSTAGES == 4 && GLDS_PER_STEP == 4 && PARK_STORES == 8, "vmcnt bookkeeping below assumes these");
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 2, wc = wave & 3;
+    uint32_t *const spare = reinterpret_cast<uint32_t *>(smem + PLDS_BYTES);
+    if (PRIO == 1 && wr == 1) __builtin_amdgcn_s_setprio(1);
+
+    const unsigned G = gridDim.x, bid = blockIdx.x, xcd = bid & 7;
+    const unsigned nblk = (G >> 3) + (xcd < (G & 7) ? 1u : 0u);
+    const unsigned P = g.mtiles * g.ntiles, q8 = P >> 3, r8 = P & 7;
+    const unsigned tx = q8 + (xcd < r8 ? 1u : 0u);
+    const unsigned basex = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+    const unsigned total = g.nplanes * tx;
+    auto tile_u = [&](unsigned i) {
+        const unsigned y = __builtin_amdgcn_readfirstlane(i / tx);
+        return y * P + basex + (i - y * tx);
+    };
+    auto claim = [&]() { return __hip_atomic_fetch_add(g.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto to_tile = [&](unsigned pos) { return pos + nblk < total ? pos + nblk : NO_TILE; };
+    unsigned ccur = (bid >> 3) < total ? (bid >> 3) : NO_TILE;
+    if (ccur == NO_TILE) return;  // block-uniform, before any barrier
+    if (tid == 0) spare[0] = to_tile(claim());
+
+    const unsigned K = g.ksteps;  // >= 6 (host)
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
+    const uint32_t lds_wave = lds_base + wave * 1024;
+    const uint32_t lane_off = wave * 1024 + lane * 16;
+    auto rsrcA = [&](const TileRef &t) { return make_rsrc(g.A + (size_t)t.j * g.planeA, (uint32_t)g.planeA); };
+    auto rsrcB = [&](const TileRef &t) { return make_rsrc(g.B + (size_t)t.j * g.planeB, (uint32_t)g.planeB); };
+    auto lo_of = [&](unsigned step) { return lds_wave + (step & (PSTAGES - 1)) * SLOT; };
+    auto rd_of = [&](unsigned step) { return smem + (step & (PSTAGES - 1)) * SLOT; };
+
+    TileRef ct = decode_tile<SUB>(g, tile_u(ccur));
+    v4si rA = rsrcA(ct), rB = rsrcB(ct);
+    constexpr unsigned D = PSTAGES - 1;
+    for (unsigned s0 = 0; s0 < D; ++s0) {
+        const uint32_t lo = lo_of(s0);
+        bglds16(rA, ct.offA + s0 * PANEL + lane_off, lo);
+        bglds16(rA, ct.offA + s0 * PANEL + lane_off + 8192, lo + 8192);
+        bglds16(rB, ct.offB + s0 * PANEL + lane_off, lo + PANEL);
+        bglds16(rB, ct.offB + s0 * PANEL + lane_off + 8192, lo + PANEL + 8192);
+    }
+    wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();  // step 0 landed (and the claim's LDS write)
+    barrier();
+
+    unsigned s = 0;
+    unsigned cnext = __builtin_amdgcn_readfirstlane(spare[0]);
+    uint32_t da = ct.offA + D * PANEL, db = ct.offB + D * PANEL;
+    Frags f;
+    AccTile acc[ACC_I][ACC_J];
+    unsigned pos = 0;  // thread 0: the queue position claimed for the tile after next
+    bool claimed = false;
+    if (wr == 1) barrier();  // group 1 falls one barrier behind, for the whole launch
+    for (unsigned r = 0;; ++r) {
+        const v4i bias = v4i{} + (g.biased ? g.bias[ct.j] : 0);
+        unsigned k = 0;
+        uint32_t na = 0, nb = 0;
+        v4si nrA = rA, nrB = rB;
+        // one k-step: reads of slot s, DMA of step s+3 (the cursor jumps to the next tile after staging this
+        // tile's last step), wait, MFMAs (the first of a tile from the bias splat), then `mid` (wave 0's publish)
+        auto step = [&](auto wait, auto first, auto mid) {
+            read_frags(f, rd_of(s), wr, wc, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t lo = lo_of(s + D);
+            bglds16(rA, da + lane_off, lo);
+            bglds16(rA, da + lane_off + 8192, lo + 8192);
+            bglds16(rB, db + lane_off, lo + PANEL);
+            bglds16(rB, db + lane_off + 8192, lo + PANEL + 8192);
+            const bool jump = k + D + 1 == K;
+            da = jump ? na : da + PANEL;
+            db = jump ? nb : db + PANEL;
+            if (jump) {  // block-uniform
+                rA = nrA;
+                rB = nrB;
+            }
+            wait();
+            barrier();
+            if constexpr (decltype(first)::value) mfma_step_first(acc, f, bias);
+            else mfma_step<PRIO>(acc, f);
+            mid();
+            barrier();
+        };
+        auto none = [] {};
+        // steps 0 and 1 (one code path for every tile: the accumulators get ONE defining MFMA): from the second
+        // tile on, the previous tile's 8 residue stores are younger than the awaited DMA
+        auto wait01 = [&] {
+            if (r > 0) wait_vm_lgkm0<GLDS_PER_STEP *(D - 1) + PARK_STORES>();
+            else wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();
+        };
+        step(wait01, std::true_type{}, [&] {
+            if (claimed) {  // group 0's MFMA interval: group 1 has read its parked residues back
+                spare[0] = to_tile(pos);
+                __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
+            }
+        });
+        ++k, ++s;
+        step(wait01, std::false_type{}, none);
+        ++k, ++s;
+        if (r > 0) cnext = __builtin_amdgcn_readfirstlane(spare[0]);  // published by thread 0 two barriers ago
+        TileRef nt = ct;
+        if (cnext != NO_TILE) {
+            nt = decode_tile<SUB>(g, tile_u(cnext));
+            na = nt.offA;
+            nb = nt.offB;
+            nrA = rsrcA(nt);
+            nrB = rsrcB(nt);
+        }
+        const unsigned kend = cnext != NO_TILE ? K : K - D;
+        for (; k < kend; ++k, ++s) step([] { wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>(); }, std::false_type{}, none);
+        for (; k < K; ++k, ++s) {  // drain of the block's last tile
+            read_frags(f, rd_of(s), wr, wc, lane);
+            __builtin_amdgcn_sched_barrier(0);
+            wait_steps_lgkm0<GLDS_PER_STEP>(k + 2 < K ? (int)(K - k - 2) : 0);
+            barrier();
+            mfma_step<PRIO>(acc, f);
+            barrier();
+        }
+
+        // ---- this group's epilogue: park interval, then store interval ----
+        claimed = tid == 0 && cnext != NO_TILE;
+        if (claimed) pos = claim();
+        int etid = tid;
+        asm volatile("" : "+v"(etid));
+        const int elane = etid & 63, gtid = etid & 255;
+        const int p = g.p[ct.j];
+        uint32_t *const park = wr == 0 ? reinterpret_cast<uint32_t *>(rd_of(s - 1)) : spare;
+        auto park_all = [&](auto &&res) {
+#pragma unroll
+            for (int i = 0; i < ACC_I; ++i)
+#pragma unroll
+                for (int jj = 0; jj < ACC_J; ++jj) {
+                    const int col = wc * 64 + acc_col(jj, elane);
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][e]) << (8 * e);
+                    const int q = elane >> 4;  // dword 4 i + q of the column (rows 16 i + 4 q ..)
+                    park[col * 32 + ((i ^ ((col >> 1) & 7)) << 2) + (q ^ ((col & 1) << 1))] = w;
+                }
+        };
+        if (g.biased && p == 256) {
+            park_all([&](int x) { return (uint32_t)x & 0xffu; });
+        } else if (g.biased) {
+            const double invp = g.invp[ct.j], pneg = -(double)p;
+            const double cneg = __builtin_fma(-0x1p52, invp, 0x1p-8);
+            park_all([&](int x) { return residue_biased_f64((uint32_t)x, invp, cneg, pneg); });
+        } else {
+            const int bar = g.barrett[ct.j];
+            const bool p256 = (p == 256);
+            park_all([&](int x) { return residue(x, p, bar, p256); });
+        }
+        __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0), vmcnt untouched
+        barrier();
+        uint8_t *out = static_cast<uint8_t *>(g.out) + ct.j * g.planeOut + ct.sb * g.subOut +
+                       (size_t)ct.tn * 256 * g.ldo + (size_t)ct.tm * 256 + wr * 128;
+#pragma unroll
+        for (int it = 0; it < PARK_STORES; ++it) {
+            const int chunk = gtid + 256 * it;
+            const int col = chunk >> 3, c = chunk & 7;
+            const uint4 v = *reinterpret_cast<const uint4 *>(park + col * 32 + ((c ^ ((col >> 1) & 7)) << 2));
+            const int pm = (col & 1) << 1;
+            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+            typedef unsigned u4v __attribute__((ext_vector_type(4)));
+            const u4v val = u4v{e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]};
+            u4v *dst = reinterpret_cast<u4v *>(out + (size_t)col * g.ldo + 16 * c);
+            if (OZ2_RES_NTS) __builtin_nontemporal_store(val, dst);
+            else *dst = val;
+        }
+        if (claimed) asm volatile("" ::"v"(pos));  // the claim returned (older than the 8 stores: vmcnt(8))
+        __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // park reads done
+        barrier();
+        if (cnext == NO_TILE) break;
+        ct = nt;
+    }
+    if (wr == 0) barrier();  // group 0 passed one barrier fewer (group 1's initial one)
+}
+
 // Exhaustive check of the two residue epilogues against exact arithmetic, every input and every
 // modulus: path 0 = biased (x in [-2^30, 2^30], the accumulator starting at bias_i), path 1 = signed
 // Barrett (every int32, conv_32i_2_8u.hpp:7-56).  Counts mismatches into *count.
@@ -965,6 +1177,18 @@ int g_prio_override = 1;  // probes: the persistent kernel's priority variant (P
 int g_epim_override = 0;  // probes: the persistent kernel's residue arithmetic (EPIM; 0 = the default)
 int g_order_override = 0;  // probes: the persistent kernel's k order (ORD; 0 = the default)
 unsigned long long *g_stamps = nullptr;  // probes: OZ2_STAMPS builds' per-wave phase sums
+// the persistent kernel's epilogue: per wave group without realignment (gemm_i8_persistent_pg_kernel) or the
+// whole block after realigning the groups (gemm_i8_persistent_kernel).  GEMMUL8_PG_EPILOGUE=0/1 (read once);
+// g_pg_override (probes) wins when >= 0.
+int g_pg_override = -1;
+static bool pg_epilogue() {
+    if (g_pg_override >= 0) return g_pg_override != 0;
+    static const bool env = [] {
+        const char *e = getenv("GEMMUL8_PG_EPILOGUE");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return env;
+}
 static int persistent_mode() {
     if (g_persistent_override >= 0) return g_persistent_override;
     static const int env = [] {
@@ -1055,7 +1279,10 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
             return e ? (unsigned)atoi(e) : 0u;
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
-        if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
+        if (pg_epilogue()) {
+            if (g.nsub == 3) launch(gemm_i8_persistent_pg_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
+            else launch(gemm_i8_persistent_pg_kernel<false, 1>, pgrid, dim3(NTHREADS), st, g);
+        } else if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 1) launch(gemm_i8_persistent_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 2) launch(gemm_i8_persistent_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
 #ifdef OZ2_EPIM_PROBES
