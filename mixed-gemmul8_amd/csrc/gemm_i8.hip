@@ -911,7 +911,9 @@ __device__ __forceinline__ void mfma_step_first(AccTile (&acc)[ACC_I][ACC_J], co
     __builtin_amdgcn_sched_barrier(0);
 }
 
-template <bool SUB, int PRIO = 1>
+// ABL (probe builds, tools/probes/persist_pg_ab.hip): 1 = residues reduced to the low byte (wrong residues), 2 = no
+// residue stores, 3 = neither park nor stores (the epilogue's barriers only)
+template <bool SUB, int PRIO = 1, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(GemmArgs g) {
     static_assert(OZ2_MFMA16, "per-group epilogue: 16x16x64 accumulator map");
     __shared__ __attribute__((aligned(1024))) int8_t smem[PLDS_BYTES + PARK_SPARE];
@@ -1043,6 +1045,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
         const int p = g.p[ct.j];
         uint32_t *const park = wr == 0 ? reinterpret_cast<uint32_t *>(rd_of(s - 1)) : spare;
         auto park_all = [&](auto &&res) {
+            if (ABL == 3) return;
 #pragma unroll
             for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
@@ -1055,7 +1058,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
                     park[col * 32 + ((i ^ ((col >> 1) & 7)) << 2) + (q ^ ((col & 1) << 1))] = w;
                 }
         };
-        if (g.biased && p == 256) {
+        if (ABL == 1 || (g.biased && p == 256)) {
             park_all([&](int x) { return (uint32_t)x & 0xffu; });
         } else if (g.biased) {
             const double invp = g.invp[ct.j], pneg = -(double)p;
@@ -1072,6 +1075,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
                        (size_t)ct.tn * 256 * g.ldo + (size_t)ct.tm * 256 + wr * 128;
 #pragma unroll
         for (int it = 0; it < PARK_STORES; ++it) {
+            if (ABL >= 2) break;
             const int chunk = gtid + 256 * it;
             const int col = chunk >> 3, c = chunk & 7;
             const uint4 v = *reinterpret_cast<const uint4 *>(park + col * 32 + ((c ^ ((col >> 1) & 7)) << 2));
@@ -1280,6 +1284,12 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
         if (pg_epilogue()) {
+#ifdef OZ2_PG_ABLATE_PROBES
+            if (g_pg_override == 2) launch(gemm_i8_persistent_pg_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
+            else if (g_pg_override == 3) launch(gemm_i8_persistent_pg_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
+            else if (g_pg_override == 4) launch(gemm_i8_persistent_pg_kernel<false, 1, 3>, pgrid, dim3(NTHREADS), st, g);
+            else
+#endif
             if (g.nsub == 3) launch(gemm_i8_persistent_pg_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
             else launch(gemm_i8_persistent_pg_kernel<false, 1>, pgrid, dim3(NTHREADS), st, g);
         } else if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
