@@ -881,6 +881,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
 #undef OZ2_STAMP
 }
 
+#ifdef OZ2_PG_PROBES
 // ---------------------------------------------------------------------------------------------
 // Persistent residue product with PER-GROUP epilogues (round 6).  The same DMA pipeline, tile queues and
 // main loop as gemm_i8_persistent_kernel, but the two wave groups (rows 0-127 / 128-255 of the tile) stay one
@@ -891,6 +892,8 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
 // (L = fragment reads + DMA issue, M = MFMAs; ' = the next tile): group 0's park runs beside group 1's last
 // MFMAs, and the two epilogues overlap each other instead of following each other with the whole block
 // waiting at four barriers.  Per tile each group passes 2K + 2 barriers.
+// MEASURED NEUTRAL (round 6, profiles/r06/epilogue_ab/): same residues, per-tile overhead within the run-to-run
+// spread of the block-epilogue kernel on three boxes; built into probe builds only (OZ2_PG_PROBES).
 // Group 0 parks in the ring slot of the tile's last step (its next writer is group 0's own DMA of the next
 // tile's step 3, issued in L'(0) after its store sweep has read the slot back), group 1 in the spare 32 KiB.
 // The accumulators are not reset: the first MFMA of each tile reads its C operand from a splat of the
@@ -1045,7 +1048,13 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
         const int p = g.p[ct.j];
         uint32_t *const park = wr == 0 ? reinterpret_cast<uint32_t *>(rd_of(s - 1)) : spare;
         auto park_all = [&](auto &&res) {
-            if (ABL == 3) return;
+            if (ABL == 3) {  // probe: the accumulators stay live (else their MFMAs are dead code)
+#pragma unroll
+                for (int i = 0; i < ACC_I; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < ACC_J; ++jj) asm volatile("" ::"v"(acc[i][jj]));
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
@@ -1095,6 +1104,8 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
     }
     if (wr == 0) barrier();  // group 0 passed one barrier fewer (group 1's initial one)
 }
+
+#endif  // OZ2_PG_PROBES
 
 // Exhaustive check of the two residue epilogues against exact arithmetic, every input and every
 // modulus: path 0 = biased (x in [-2^30, 2^30], the accumulator starting at bias_i), path 1 = signed
@@ -1181,18 +1192,12 @@ int g_prio_override = 1;  // probes: the persistent kernel's priority variant (P
 int g_epim_override = 0;  // probes: the persistent kernel's residue arithmetic (EPIM; 0 = the default)
 int g_order_override = 0;  // probes: the persistent kernel's k order (ORD; 0 = the default)
 unsigned long long *g_stamps = nullptr;  // probes: OZ2_STAMPS builds' per-wave phase sums
-// the persistent kernel's epilogue: per wave group without realignment (gemm_i8_persistent_pg_kernel) or the
-// whole block after realigning the groups (gemm_i8_persistent_kernel).  GEMMUL8_PG_EPILOGUE=0/1 (read once);
-// g_pg_override (probes) wins when >= 0.
-int g_pg_override = -1;
-static bool pg_epilogue() {
-    if (g_pg_override >= 0) return g_pg_override != 0;
-    static const bool env = [] {
-        const char *e = getenv("GEMMUL8_PG_EPILOGUE");
-        return e ? atoi(e) != 0 : false;
-    }();
-    return env;
-}
+#ifdef OZ2_PG_PROBES
+// probe builds: the persistent kernel's epilogue per wave group (gemm_i8_persistent_pg_kernel; g_pg_override 1,
+// ablations 2-4) or the default block epilogue (0)
+int g_pg_override = 0;
+static bool pg_epilogue() { return g_pg_override != 0; }
+#endif
 static int persistent_mode() {
     if (g_persistent_override >= 0) return g_persistent_override;
     static const int env = [] {
@@ -1283,16 +1288,16 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
             return e ? (unsigned)atoi(e) : 0u;
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
+#ifdef OZ2_PG_PROBES
         if (pg_epilogue()) {
-#ifdef OZ2_PG_ABLATE_PROBES
             if (g_pg_override == 2) launch(gemm_i8_persistent_pg_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
             else if (g_pg_override == 3) launch(gemm_i8_persistent_pg_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
             else if (g_pg_override == 4) launch(gemm_i8_persistent_pg_kernel<false, 1, 3>, pgrid, dim3(NTHREADS), st, g);
-            else
-#endif
-            if (g.nsub == 3) launch(gemm_i8_persistent_pg_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
+            else if (g.nsub == 3) launch(gemm_i8_persistent_pg_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
             else launch(gemm_i8_persistent_pg_kernel<false, 1>, pgrid, dim3(NTHREADS), st, g);
-        } else if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
+        } else
+#endif
+        if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 1) launch(gemm_i8_persistent_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 2) launch(gemm_i8_persistent_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
 #ifdef OZ2_EPIM_PROBES

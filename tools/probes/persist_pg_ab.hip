@@ -4,7 +4,8 @@
 // operand bytes, m = n = argv[2] (default 8192), N = argv[1] planes (default 14), k in {1024 ... 16384}.
 // Prints per variant the ns per GMAC for each k and the fit Y + X / ksteps (X / Y = the per-tile overhead in k-step
 // equivalents, as tools/probes/persist_ksweep.hip), and checks that both variants write identical residue planes.
-#define OZ2_PG_ABLATE_PROBES 1
+// argv[4] = 5 adds the ablations of variant 1: residues reduced to the low byte, no residue stores, no park / stores.
+#define OZ2_PG_PROBES 1
 #include "../../mixed-gemmul8_amd/csrc/gemm_i8.hip"
 #include <algorithm>
 #include <cstdio>
