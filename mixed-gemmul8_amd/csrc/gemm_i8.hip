@@ -558,6 +558,191 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Small-launch form (round 6): 128 x 128 output tiles, 256 threads = 4 waves (2 x 2, one per SIMD, each 64 x 64 =
+// 4 x 4 tiles of 16 x 16), a 4-slot ring of 16 KiB k-steps (64 KiB: two blocks per CU).  For launches with few
+// 256 x 256 tiles per CU (1024^3: 224 tiles on 256 CUs, the accurate-mode bound product of a 1024^2 or 2048^2
+// problem: 16 or 64 tiles) the 256-tile kernels leave CUs idle and expose each block's first-data latency and
+// epilogue; four times the blocks, two co-resident per CU, hide one block's epilogue and DMA waits under the
+// other's MFMAs.  The operand panels are the same 256-vector panels: a 128-row half is blocks 4h..4h+3 of both
+// 32-deep halves (two 4 KiB runs per panel), staged by LDS-DMA as 16 pieces of 1 KiB per k-step (4 per wave).
+// Per k-step and wave: wait (step t+1 landed, fragments of t in registers), barrier, fragment reads of t+1,
+// LDS-DMA of t+4 into the slot of t, 16 MFMAs of t -- the reads of the next step run under this step's MFMAs.
+constexpr int SM_THREADS = 256;
+constexpr int SM_SLOT = PANEL;           // 8 KiB A half-panel + 8 KiB B half-panel
+constexpr int SM_STAGES = 4;
+constexpr int SM_LDS = SM_STAGES * SM_SLOT;  // 64 KiB
+struct SmFrags {
+    v4i a[4];
+    v4i b[4];
+};
+// the half-panel in LDS: [s:2][blk:4][h:2][r:32][16 B] (4 KiB per s); lane l = r16 + 16 q reads the 16 k-bytes
+// 16 q.. of vector r16 of a 16-row group, as read_frags
+__device__ __forceinline__ void sm_read_frags(SmFrags &f, const int8_t *slot, int wr, int wc, int lane) {
+    const int q = lane >> 4;
+    const int8_t *base = slot + (q >> 1) * 4096 + ((q & 1) * 32 + (lane & 15)) * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)  // rows 16 i.. of the wave's 64: block wr*2 + i/2, half i&1
+        f.a[i] = *reinterpret_cast<const v4i *>(base + (wr * 2 + (i >> 1)) * 1024 + (i & 1) * 256);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj)
+        f.b[jj] = *reinterpret_cast<const v4i *>(base + 8192 + (wc * 2 + (jj >> 1)) * 1024 + (jj & 1) * 256);
+}
+__device__ __forceinline__ void sm_mfma(v4i (&acc)[4][4], const SmFrags &f) {
+#pragma unroll
+    for (int x = 0; x < 16; ++x) {
+        const int i = x >> 2, jj = x & 3;
+        acc[i][jj] = __builtin_amdgcn_mfma_i32_16x16x64_i8(f.a[i], f.b[jj], acc[i][jj], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int EPI, bool SUB = false>
+__global__ __launch_bounds__(SM_THREADS, 2) void gemm_i8_small_kernel(GemmArgs g) {
+    static_assert(OZ2_MFMA16, "small tiles: 16x16x64 accumulator map");
+    __shared__ __attribute__((aligned(1024))) int8_t smem[SM_LDS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = wave >> 1, wc = wave & 1;
+    const unsigned j = SUB ? blockIdx.y / 3 : blockIdx.y;
+    const unsigned sb = SUB ? blockIdx.y - 3 * j : 0;
+
+    // XCD-aware bijective remap (as gemm_i8_kernel), grouped raster of 8 row tiles: the ~64 co-resident tiles
+    // of an XCD (two per CU) share 8 A and 8 B half-panels
+    const unsigned mt2 = 2 * g.mtiles, nt2 = 2 * g.ntiles;
+    const unsigned nwg = gridDim.x, bid = blockIdx.x;
+    const unsigned xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const unsigned wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    constexpr unsigned GM = 8;
+    const unsigned grp = wgid / (GM * nt2);
+    const unsigned gm = min(GM, mt2 - grp * GM);
+    const unsigned idx = wgid - grp * GM * nt2;
+    const unsigned tm2 = grp * GM + idx % gm, tn2 = idx / gm;
+    const unsigned tm = tm2 >> 1, hm = tm2 & 1, tn = tn2 >> 1, hn = tn2 & 1;
+
+    // this wave's LDS-DMA pieces: A and B pieces w (s = 0) and w + 4 (s = 1) of the half-panels
+    const v4si rA = make_rsrc(g.A + j * g.planeA, (uint32_t)g.planeA);
+    const v4si rB = make_rsrc(g.B + j * g.planeB, (uint32_t)g.planeB);
+    const uint32_t oA = (uint32_t)(sb * g.subA + ((size_t)tm * g.kstride + g.k0) * PANEL) + (4 * hm + wave) * 1024 + lane * 16;
+    const uint32_t oB = (uint32_t)(sb * g.subB + ((size_t)tn * g.kstride + g.k0) * PANEL) + (4 * hn + wave) * 1024 + lane * 16;
+    const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
+    const uint32_t lds_wave = lds_base + wave * 1024;
+    auto stage = [&](unsigned ks) {
+        const uint32_t go = ks * (uint32_t)PANEL, lo = lds_wave + (ks & (SM_STAGES - 1)) * SM_SLOT;
+        bglds16(rA, oA + go, lo);
+        bglds16(rA, oA + go + 8192, lo + 4096);
+        bglds16(rB, oB + go, lo + 8192);
+        bglds16(rB, oB + go + 8192, lo + 8192 + 4096);
+    };
+
+    v4i acc[4][4];
+    const int acc0 = ((EPI == (int)Epi::RESIDUE) && g.biased) ? g.bias[j] : 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) acc[i][jj] = v4i{} + acc0;
+
+    const unsigned K = g.ksteps;
+    SmFrags fa, fb;
+    if (K > 0) {
+        // prologue: steps 0..3 in flight (the ring's four slots), step 0 landed, its fragments read
+        for (unsigned s0 = 0; s0 < SM_STAGES; ++s0)
+            if (s0 < K) stage(s0);
+        wait_steps_lgkm0<GLDS_PER_STEP>((int)min(K, (unsigned)SM_STAGES) - 1);
+        barrier();
+        sm_read_frags(fa, smem, wr, wc, lane);
+        for (unsigned t = 0; t < K; t += 2) {
+            // step t (fragments in fa): wait for step t+1 (steps t+2, t+3 may fly) and fa, barrier, read t+1,
+            // stage t+4 into the slot of t, MFMAs of t; then the same for t+1 with fa / fb swapped
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const unsigned tt = t + u;
+                if (tt >= K) break;
+                SmFrags &cur = u == 0 ? fa : fb, &nxt = u == 0 ? fb : fa;
+                const int fly = (int)min(K - 1 - min(tt + 1, K - 1), 2u);  // steps younger than tt+1 in flight
+                wait_steps_lgkm0<GLDS_PER_STEP>(fly);
+                barrier();
+                if (tt + 1 < K) sm_read_frags(nxt, smem + ((tt + 1) & (SM_STAGES - 1)) * SM_SLOT, wr, wc, lane);
+                __builtin_amdgcn_sched_barrier(0);
+                if (tt + SM_STAGES < K) stage(tt + SM_STAGES);
+                sm_mfma(acc, cur);
+            }
+        }
+    }
+    barrier();  // every wave's MFMAs issued and its reads of the ring done: the epilogue reuses slot 0
+
+    if constexpr (EPI == (int)Epi::RESIDUE) {
+        const int p = g.p[j];
+        uint32_t *park = reinterpret_cast<uint32_t *>(smem);  // [128 cols][32 dwords], swizzled as the pg kernel
+        auto park_all = [&](auto &&res) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const int col = wc * 64 + acc_col(jj, lane), q = lane >> 4, c = wr * 4 + i;
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][e]) << (8 * e);
+                    park[col * 32 + ((c ^ ((col >> 1) & 7)) << 2) + (q ^ ((col & 1) << 1))] = w;
+                }
+        };
+        if (g.biased && p == 256) {
+            park_all([&](int x) { return (uint32_t)x & 0xffu; });
+        } else if (g.biased) {
+            const double invp = g.invp[j], pneg = -(double)p;
+            const double cneg = __builtin_fma(-0x1p52, invp, 0x1p-8);
+            park_all([&](int x) { return residue_biased_f64((uint32_t)x, invp, cneg, pneg); });
+        } else {
+            const int bar = g.barrett[j];
+            const bool p256 = (p == 256);
+            park_all([&](int x) { return residue(x, p, bar, p256); });
+        }
+        __syncthreads();
+        uint8_t *out = static_cast<uint8_t *>(g.out) + j * g.planeOut + sb * g.subOut + (size_t)tn2 * 128 * g.ldo +
+                       (size_t)tm2 * 128;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {  // 128 columns x 8 chunks of 16 B
+            const int chunk = tid + SM_THREADS * it;
+            const int col = chunk >> 3, c = chunk & 7;
+            const uint4 v = *reinterpret_cast<const uint4 *>(park + col * 32 + ((c ^ ((col >> 1) & 7)) << 2));
+            const int pm = (col & 1) << 1;
+            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+            *reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * c) = make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
+        }
+    } else if constexpr (EPI == (int)Epi::BOUND) {
+        int32_t *rmax = reinterpret_cast<int32_t *>(smem);
+        int32_t *cmax = rmax + 128;
+        rmax[tid & 127] = 0;  // (threads 0-127 and 128-255 write the same zeros)
+        cmax[tid & 127] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+                int v = 0;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) v = max(v, abs(acc[i][jj][rr]));
+#pragma unroll
+                for (int d = 8; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 16));
+                if ((lane & 15) == 0) atomicMax(&rmax[wr * 64 + acc_row(i, rr, lane)], v);
+            }
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            int v = 0;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int rr = 0; rr < 4; ++rr) v = max(v, abs(acc[i][jj][rr]));
+#pragma unroll
+            for (int d = 16; d < 64; d <<= 1) v = max(v, __shfl_xor(v, d));
+            if (lane < 16) atomicMax(&cmax[wc * 64 + acc_col(jj, lane)], v);
+        }
+        __syncthreads();
+        if (tid < 128) atomicMax(&g.rowmax[tm2 * 128 + tid], rmax[tid]);
+        else atomicMax(&g.colmax[tn2 * 128 + tid - 128], cmax[tid - 128]);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Persistent form of the residue product (buffer DMA; real operands and Karatsuba sub-products).
 // One block per CU.  The k-steps of a block's consecutive tiles form ONE pipeline: the LDS-DMA
 // runs D steps ahead across tile boundaries, so the next tile's first panels land while the
@@ -1198,6 +1383,18 @@ unsigned long long *g_stamps = nullptr;  // probes: OZ2_STAMPS builds' per-wave 
 int g_pg_override = 0;
 static bool pg_epilogue() { return g_pg_override != 0; }
 #endif
+// GEMMUL8_SMALL_TILES: 0 = never the 128 x 128 kernel, 1 = wherever it applies, unset (2) = below
+// SMALL_TILES_BELOW 256 x 256 tiles per CU.  g_small_override (probes) wins when >= 0.
+int g_small_override = -1;
+constexpr unsigned SMALL_TILES_BELOW = 2;
+static int small_tiles_mode() {
+    if (g_small_override >= 0) return g_small_override;
+    static const int env = [] {
+        const char *e = getenv("GEMMUL8_SMALL_TILES");
+        return e ? atoi(e) : 2;
+    }();
+    return env;
+}
 static int persistent_mode() {
     if (g_persistent_override >= 0) return g_persistent_override;
     static const int env = [] {
@@ -1275,6 +1472,22 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     const unsigned ntiles_all = (unsigned)(L.mtiles * L.ntiles) * nplanes * g.nsub;
     const unsigned ncu = device_cu_count();
     const int pmode = persistent_mode();
+    // small launches (fewer than SMALL_TILES_BELOW 256 x 256 tiles per CU): 128 x 128 tiles, two blocks per CU
+    // (gemm_i8_small_kernel).  GEMMUL8_SMALL_TILES=0 never, 1 wherever it applies (residue and bound products
+    // over buffer descriptors), unset by that rule unless GEMMUL8_PERSISTENT forces a 256-tile kernel.
+    const int smode = small_tiles_mode();
+    if ((epi == Epi::RESIDUE || epi == Epi::BOUND) && buf &&
+        (smode == 1 || (smode == 2 && pmode == 2 && ntiles_all < SMALL_TILES_BELOW * ncu))) {
+        const dim3 sgrid((unsigned)(4 * L.mtiles * L.ntiles), nplanes * g.nsub);
+        if (epi == Epi::RESIDUE) {
+            g_last_residue_kernel.store(4, std::memory_order_relaxed);
+            if (g.nsub == 3) launch(gemm_i8_small_kernel<0, true>, sgrid, dim3(SM_THREADS), st, g);
+            else launch(gemm_i8_small_kernel<0, false>, sgrid, dim3(SM_THREADS), st, g);
+        } else {
+            launch(gemm_i8_small_kernel<1, false>, sgrid, dim3(SM_THREADS), st, g);
+        }
+        return;
+    }
     if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 3 * ncu)) {
         g_last_residue_kernel.store(2, std::memory_order_relaxed);
         g.nplanes = nplanes * g.nsub;

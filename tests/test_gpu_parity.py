@@ -725,6 +725,73 @@ def test_persistent_default_matches_one_tile():
             assert np.array_equal(outs[0][k].view(np.uint64), outs[1][k].view(np.uint64)), k
 
 
+def test_small_tiles_match_one_tile():
+    """The 128 x 128-tile product kernel (gemm_i8_small_kernel; the default below 2 tiles of 256 x 256 per CU):
+    C bit-identical to the 256-tile one-tile kernel (GEMMUL8_SMALL_TILES=0 GEMMUL8_PERSISTENT=0) and the rule's
+    default, child processes, at 1024^3 (224 tiles, the default rule), odd shapes with partial 128-tiles, k
+    from 1 k-step to 33, accurate mode (the bound product runs the small kernel too), f32, Karatsuba complex
+    sub-products, and with the kernel forced wherever it applies (GEMMUL8_SMALL_TILES=1: 2048^3, 3.5 tiles of
+    256 x 256 per CU); the oracle checks the forced small kernel's slices, residues and C at small shapes"""
+    import subprocess
+    import tempfile
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    code = ("import sys, numpy as np, torch; sys.path[:0] = sys.argv[1:3]\n"
+            "import gemmul8 as G\n"
+            "out = sys.argv[3]; res = {}\n"
+            "cases = ((1024, 1024, 1024, 14, True, 'd', 0), (300, 200, 64, 14, True, 'd', 0),\n"
+            "         (900, 130, 2100, 14, True, 'd', 0), (1024, 1024, 1024, 14, False, 'd', 0),\n"
+            "         (700, 540, 333, 9, False, 'd', 0), (520, 270, 400, 7, True, 'f', 0),\n"
+            "         (1024, 300, 3072, 12, True, 'z', 3), (2048, 2048, 2048, 14, True, 'd', 0))\n"
+            "for m, n, k, N, fast, t, ct in cases:\n"
+            "    dt = {'d': torch.float64, 'f': torch.float32, 'z': torch.complex128}[t]\n"
+            "    g = torch.Generator(device='cuda'); g.manual_seed(m + n + k)\n"
+            "    A = torch.randn((k, m), dtype=dt, device='cuda', generator=g)\n"
+            "    B = torch.randn((n, k), dtype=dt, device='cuda', generator=g)\n"
+            "    C = torch.empty((n, m), dtype=dt, device='cuda')\n"
+            "    W = G.alloc_work(m, n, k, N, ct)\n"
+            "    G.gemm(0, 0, m, n, k, 1.0, A, m, B, k, 0.0, C, m, N, fast, W, ct)\n"
+            "    res[f'{m}_{n}_{k}_{N}_{fast}_{t}'] = C.cpu().numpy()\n"
+            "    res[f'{m}_{n}_{k}_{N}_{fast}_{t}_kernel'] = np.array([G.last_products_kernel()])\n"
+            "np.savez(out, **res)\n")
+    modes = {"onetile": {"GEMMUL8_SMALL_TILES": "0", "GEMMUL8_PERSISTENT": "0"}, "default": {},
+             "forced": {"GEMMUL8_SMALL_TILES": "1"}}
+    with tempfile.TemporaryDirectory() as d:
+        outs = {}
+        for name, extra in modes.items():
+            out = os.path.join(d, f"{name}.npz")
+            env = {kk: v for kk, v in os.environ.items() if kk not in ("GEMMUL8_SMALL_TILES", "GEMMUL8_PERSISTENT")}
+            env.update(extra)
+            r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "mixed-gemmul8_amd"), tdir, out],
+                               env=env, capture_output=True, text=True, timeout=300)
+            assert r.returncode == 0, (name, r.stderr[-3000:])
+            outs[name] = np.load(out)
+        for key in outs["onetile"].files:
+            if key.endswith("_kernel"):
+                continue
+            for name in ("default", "forced"):
+                assert np.array_equal(outs["onetile"][key].view(np.uint8), outs[name][key].view(np.uint8)), (name, key)
+        assert str(outs["forced"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
+        assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
+        assert str(outs["default"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_persistent_kernel"
+        assert str(outs["onetile"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
+    code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
+            "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
+            "rng = np.random.default_rng(29)\n"
+            "check_full(randmat_np(rng, 300, 513), randmat_np(rng, 513, 260), 14)\n"
+            "check_full(randmat_np(rng, 130, 64), randmat_np(rng, 64, 129), 14)\n"
+            "check_full(randmat_np(rng, 700, 333), randmat_np(rng, 333, 530), 9, fast=False)\n"
+            "check_full(randmat_np(rng, 520, 400, dtype=np.float32), randmat_np(rng, 400, 270, dtype=np.float32), 7)\n"
+            "check_full(randmat_np(rng, 300, 333, dtype=np.complex128), randmat_np(rng, 333, 290, dtype=np.complex128), 12, ctype=3)\n"
+            "print('OK')")
+    for extra in ({"GEMMUL8_SMALL_TILES": "1", "GEMMUL8_CPLX_PRODUCTS": "karatsuba"},
+                  {"GEMMUL8_SMALL_TILES": "0", "GEMMUL8_PERSISTENT": "0"}):
+        env = dict(os.environ, **extra)
+        r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "OK" in r.stdout, (extra, r.stderr[-3000:])
+
+
 def test_persistent_planes_beyond_4gib():
     """A launch whose 14 A slice planes span more than 4 GiB (m = 20480, k = 15360: 315 MB per plane):
     the persistent kernel addresses each modulus's plane with its own buffer descriptor and switches

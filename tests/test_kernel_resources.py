@@ -19,6 +19,8 @@ pytestmark = pytest.mark.skipif(not shutil.which("llvm-readelf", path="/opt/rocm
 FLOORS = {
     "oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>": 2,  # cfg2/3/4 products: 512 threads, 160 KiB LDS, 1 block per CU
     "oz2::gemm_i8_persistent_kernel<true, 1, 0, 0>": 2,  # cfg5 (Karatsuba sub-products)
+    "oz2::gemm_i8_small_kernel<0, false>": 2,       # small launches: 256 threads, 64 KiB LDS, 2 blocks per CU
+    "oz2::gemm_i8_small_kernel<1, false>": 2,       # the accurate-mode bound product of small problems
     "oz2::crt_kernel<0, false, 14u, false, 8>": 5,     # cfg2/3 CRT
     "oz2::crt_kernel<0, false, 10u, false, 8>": 5,     # cfg4 CRT
     "oz2::crt_kernel<2, false, 12u, true, 8>": 3,      # cfg5 CRT (Karatsuba residues)
