@@ -203,6 +203,17 @@ int gemmul8_dd_gemm(void *stream, size_t m, size_t n, size_t k, const double *A,
                     double *C2);
 /* err[i] = |C[i] - (C1[i] + C2[i])| / |C1[i] + C2[i]| evaluated in double-double (eval.hpp:317-338). */
 int gemmul8_relerr_dd(void *stream, size_t count, const double *C, const double *C1, const double *C2, double *err);
+/* the reference drivers' timing loop (GEMMul8/testing/test_double.cu:422-431) in native code: `iters` calls of
+ * gemmul8_gemm, each bracketed by hipDeviceSynchronize and the host clock; *sec = mean seconds per call,
+ * phase_ns[4] = mean phase times (NULL: not returned) */
+int gemmul8_time_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                      int type_c, const void *alpha, const void *A, size_t lda, const void *B, size_t ldb,
+                      const void *beta, void *C, size_t ldc, unsigned num_moduli, int fastmode, void *work,
+                      int compute_type, int iters, double *sec, double *phase_ns);
+/* the same loop around the vendor GEMM of the drivers (test_double.cu:318-331): hipblasGemmEx op N / N, alpha 1,
+ * beta 0, every operand of `type`, lda = m, ldb = k, ldc = m */
+int gemmul8_time_vendor_gemm(void *stream, int type, size_t m, size_t n, size_t k, const void *A, const void *B,
+                             void *C, int iters, double *sec);
 /* Data-bound ceiling of the int8 products: TOPS of the better of v_mfma_i32_32x32x32_i8 and
  * v_mfma_i32_16x16x64_i8 alone on uniformly random operand bytes held in registers (2 waves per
  * SIMD, the ops of `iters` x 64 32x32x32 MFMAs per wave); synchronises. */

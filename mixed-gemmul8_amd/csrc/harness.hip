@@ -6,8 +6,15 @@
 //  * gemmul8_dd_gemm: double-double reference product (testing/eval.hpp:265-308),
 //    TwoProd + double-double accumulation, LDS-tiled.
 //  * gemmul8_relerr_dd: |C - Cref| / |Cref| in double-double (eval.hpp:317-338).
+//  * gemmul8_time_gemm / gemmul8_time_vendor_gemm: the drivers' timing loop in native code
+//    (test_double.cu:318-331, 422-431): per call a device sync, the host clock, the call, a device sync,
+//    the clock -- without the Python binding's per-call overhead, for the emulation and the vendor GEMM alike.
 #include <hip/hip_runtime.h>
+#include <hipblas/hipblas.h>
 #include <hiprand/hiprand_kernel.h>
+
+#include <chrono>
+#include <mutex>
 
 #include "../../include/gemmul8_c.h"
 
@@ -251,6 +258,73 @@ int gemmul8_dd_gemm(void *stream, size_t m, size_t n, size_t k, const double *A,
     dim3 grid((unsigned)((m + 63) / 64), (unsigned)((n + 63) / 64));
     oz2h::dd_gemm_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(m, n, k, A, B, C1, C2);
     return hipGetLastError() == hipSuccess ? GEMMUL8_OK : GEMMUL8_E_HIP;
+}
+
+int gemmul8_time_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
+                      int type_c, const void *alpha, const void *A, size_t lda, const void *B, size_t ldb,
+                      const void *beta, void *C, size_t ldc, unsigned num_moduli, int fastmode, void *work,
+                      int compute_type, int iters, double *sec, double *phase_ns) {
+    if (iters <= 0 || !sec) return GEMMUL8_E_SIZE;
+    double ph[4] = {0, 0, 0, 0}, total = 0.0;
+    for (int it = 0; it < iters; ++it) {
+        if (hipDeviceSynchronize() != hipSuccess) return GEMMUL8_E_HIP;
+        double p[4] = {0, 0, 0, 0};
+        const auto t0 = std::chrono::steady_clock::now();
+        const int rc = gemmul8_gemm(stream, op_a, op_b, m, n, k, type_a, type_b, type_c, alpha, A, lda, B, ldb, beta,
+                                    C, ldc, num_moduli, fastmode, work, compute_type, p);
+        if (hipDeviceSynchronize() != hipSuccess) return GEMMUL8_E_HIP;
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc != GEMMUL8_OK) return rc;
+        total += std::chrono::duration<double>(t1 - t0).count();
+        for (int i = 0; i < 4; ++i) ph[i] += p[i];
+    }
+    *sec = total / iters;
+    if (phase_ns)
+        for (int i = 0; i < 4; ++i) phase_ns[i] = ph[i] / iters;
+    return GEMMUL8_OK;
+}
+
+// the vendor routine of the drivers: hipblasGemmEx, op N / N, alpha = 1, beta = 0, column-major operands of one
+// type (GEMMUL8_R_64F: DGEMM, R_32F: SGEMM, C_32F: CGEMM, C_64F: ZGEMM) with lda = m, ldb = k, ldc = m
+int gemmul8_time_vendor_gemm(void *stream, int type, size_t m, size_t n, size_t k, const void *A, const void *B,
+                             void *C, int iters, double *sec) {
+    static std::mutex mu;
+    static hipblasHandle_t handle = nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (iters <= 0 || !sec) return GEMMUL8_E_SIZE;
+    if (!handle && hipblasCreate(&handle) != HIPBLAS_STATUS_SUCCESS) return GEMMUL8_E_HIP;
+    if (hipblasSetStream(handle, static_cast<hipStream_t>(stream)) != HIPBLAS_STATUS_SUCCESS) return GEMMUL8_E_HIP;
+    hipDataType dt;
+    hipblasComputeType_t ct;
+    switch (type) {
+    case GEMMUL8_R_64F: dt = HIP_R_64F; ct = HIPBLAS_COMPUTE_64F; break;
+    case GEMMUL8_R_32F: dt = HIP_R_32F; ct = HIPBLAS_COMPUTE_32F; break;
+    case GEMMUL8_C_64F: dt = HIP_C_64F; ct = HIPBLAS_COMPUTE_64F; break;
+    case GEMMUL8_C_32F: dt = HIP_C_32F; ct = HIPBLAS_COMPUTE_32F; break;
+    default: return GEMMUL8_E_TYPES;
+    }
+    const double one_d[2] = {1.0, 0.0}, zero_d[2] = {0.0, 0.0};
+    const float one_f[2] = {1.0f, 0.0f}, zero_f[2] = {0.0f, 0.0f};
+    const bool dbl = type == GEMMUL8_R_64F || type == GEMMUL8_C_64F;
+    const void *al = dbl ? (const void *)one_d : (const void *)one_f;
+    const void *be = dbl ? (const void *)zero_d : (const void *)zero_f;
+    auto call = [&] {
+        return hipblasGemmEx(handle, HIPBLAS_OP_N, HIPBLAS_OP_N, (int)m, (int)n, (int)k, al, A, dt, (int)m, B, dt,
+                             (int)k, be, C, dt, (int)m, ct, HIPBLAS_GEMM_DEFAULT);
+    };
+    if (call() != HIPBLAS_STATUS_SUCCESS) return GEMMUL8_E_HIP;  // (the drivers' accuracy call precedes the loop)
+    double total = 0.0;
+    for (int it = 0; it < iters; ++it) {
+        if (hipDeviceSynchronize() != hipSuccess) return GEMMUL8_E_HIP;
+        const auto t0 = std::chrono::steady_clock::now();
+        const hipblasStatus_t rc = call();
+        if (hipDeviceSynchronize() != hipSuccess) return GEMMUL8_E_HIP;
+        const auto t1 = std::chrono::steady_clock::now();
+        if (rc != HIPBLAS_STATUS_SUCCESS) return GEMMUL8_E_HIP;
+        total += std::chrono::duration<double>(t1 - t0).count();
+    }
+    *sec = total / iters;
+    return GEMMUL8_OK;
 }
 
 int gemmul8_relerr_dd(void *stream, size_t count, const double *C, const double *C1, const double *C2, double *err) {

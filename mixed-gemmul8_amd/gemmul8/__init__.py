@@ -61,6 +61,10 @@ def _load():
     lib.gemmul8_randmat.argtypes = [p, i, sz, sz, p, ctypes.c_double, ctypes.c_ulonglong]
     lib.gemmul8_dd_gemm.argtypes = [p, sz, sz, sz, p, p, p, p]
     lib.gemmul8_relerr_dd.argtypes = [p, sz, p, p, p, p]
+    lib.gemmul8_time_gemm.restype = i
+    lib.gemmul8_time_gemm.argtypes = [p, i, i, sz, sz, sz, i, i, i, p, p, sz, p, sz, p, p, sz, u, i, p, i, i, d, d]
+    lib.gemmul8_time_vendor_gemm.restype = i
+    lib.gemmul8_time_vendor_gemm.argtypes = [p, i, sz, sz, sz, p, p, p, i, d]
     lib.gemmul8_set_epilogue.argtypes = [i]
     lib.gemmul8_set_epilogue.restype = i
     lib.gemmul8_get_epilogue.argtypes = []
@@ -143,6 +147,30 @@ def gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fas
                               work.data_ptr(), computeType, pt)
     _check(rc)
     return list(pt) if phase_times else None
+
+
+def time_gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc, num_moduli, fastmode, work, iters,
+              computeType=REAL_DEFAULT, stream=None):
+    """The reference drivers' timing loop in native code (test_double.cu:422-431): `iters` gemm calls, each
+    between two device syncs and the host clock.  Returns (seconds per call, the 4 mean phase times in ns)."""
+    ta, tb, tc = _DTYPE[A.dtype], _DTYPE[B.dtype], _DTYPE[C.dtype]
+    al, be = _scalar(alpha, C.dtype), _scalar(beta, C.dtype)
+    sec, pt = ctypes.c_double(), (ctypes.c_double * 4)()
+    _check(lib.gemmul8_time_gemm(_stream(stream), opA, opB, m, n, k, ta, tb, tc, al.ptr, A.data_ptr(), lda,
+                                 B.data_ptr(), ldb, be.ptr, C.data_ptr(), ldc, num_moduli, int(bool(fastmode)),
+                                 work.data_ptr(), computeType, iters, ctypes.byref(sec), pt))
+    return sec.value, list(pt)
+
+
+def time_vendor_gemm(m, n, k, A, B, C, iters, stream=None):
+    """The same loop around hipblasGemmEx (op N / N, alpha 1, beta 0, lda = m, ldb = k, ldc = m) on column-major
+    A (m x k), B (k x n), C (m x n) of one dtype: the drivers' DGEMM / SGEMM / CGEMM rows.  Seconds per call."""
+    if not (A.dtype == B.dtype == C.dtype):
+        raise TypeError("time_vendor_gemm: A, B and C must share one dtype")
+    sec = ctypes.c_double()
+    _check(lib.gemmul8_time_vendor_gemm(_stream(stream), _DTYPE[C.dtype], m, n, k, A.data_ptr(), B.data_ptr(),
+                                        C.data_ptr(), iters, ctypes.byref(sec)))
+    return sec.value
 
 
 # ---- phase entry points (gemm == split + products + recombine; used by gemmul8.dist) ----

@@ -165,24 +165,32 @@ def flops_check(t, out, args):
             P.vendor()
             sync()
             emax, emed = relerr(P.C, P.C1, P.C2)
-            tt = timed(P.vendor, args.iters)
+            # the drivers' loop (device sync + host clock around each call) in native code, as the reference's
+            # C++ drivers time it: no Python call overhead on either side
+            tt = G.time_vendor_gemm(m, n, k, P.vA, P.vB, P.C, args.iters) if args.native_timing else \
+                timed(P.vendor, args.iters)
             f.write(f"{phi:e},{m},{n},{k},{vend},{emax:e},{emed:e},{flops / tt * 1e-12:e},{tt:e},,,,,\n")
             for fast, lab in ((True, "OS2-fast"), (False, "OS2-accu")):
                 for N in args.moduli:
                     P.emulate(N, fast, work)
                     sync()
                     emax, emed = relerr(P.C, P.C1, P.C2)
-                    ph = [0.0] * 4
-                    tt = 0.0
-                    for _ in range(args.iters):
-                        sync()
-                        t0 = time.perf_counter()
-                        p = P.emulate(N, fast, work, phases=True)
-                        sync()
-                        tt += time.perf_counter() - t0
-                        ph = [a + b for a, b in zip(ph, p)]
-                    tt /= args.iters
-                    ph = [x / args.iters * 1e-9 for x in ph]
+                    if args.native_timing:
+                        tt, ph = G.time_gemm(G.OP_N, G.OP_N, m, n, k, 1.0, P.A, m, P.B, k, 0.0, P.C, m, N, fast,
+                                             work, args.iters, P.ct)
+                        ph = [x * 1e-9 for x in ph]
+                    else:
+                        ph = [0.0] * 4
+                        tt = 0.0
+                        for _ in range(args.iters):
+                            sync()
+                            t0 = time.perf_counter()
+                            p = P.emulate(N, fast, work, phases=True)
+                            sync()
+                            tt += time.perf_counter() - t0
+                            ph = [a + b for a, b in zip(ph, p)]
+                        tt /= args.iters
+                        ph = [x / args.iters * 1e-9 for x in ph]
                     f.write(f"{phi:e},{m},{n},{k},{lab}-{N},{emax:e},{emed:e},{flops / tt * 1e-12:e},{tt:e},"
                             + "".join(f"{x:e}," for x in ph) + "\n")
                 f.flush()
@@ -262,7 +270,10 @@ def main(argv=None):
     ap.add_argument("--phi", type=float, nargs="+", default=None, help="default: the driver's list")
     ap.add_argument("--moduli", type=int, nargs="+", default=None, help="default: the driver's list")
     ap.add_argument("--iters", type=int, default=100)
+    ap.add_argument("--python-timing", action="store_true",
+                    help="time each call from Python (per-call binding overhead included) instead of the native loop")
     args = ap.parse_args(argv)
+    args.native_timing = not args.python_timing
     args.phi = args.phi or TYPES[args.type][3]
     args.moduli = args.moduli or TYPES[args.type][4]
     args.stamp = datetime.datetime.now().strftime("%Y-%m-%d_%H-%M-%S")
