@@ -1383,10 +1383,9 @@ unsigned long long *g_stamps = nullptr;  // probes: OZ2_STAMPS builds' per-wave 
 int g_pg_override = 0;
 static bool pg_epilogue() { return g_pg_override != 0; }
 #endif
-// GEMMUL8_SMALL_TILES: 0 = never the 128 x 128 kernel, 1 = wherever it applies, unset (2) = below
-// SMALL_TILES_BELOW 256 x 256 tiles per CU.  g_small_override (probes) wins when >= 0.
+// GEMMUL8_SMALL_TILES: 0 = never the 128 x 128 kernel, 1 = wherever it applies, unset (2) = the rule in
+// gemm_i8.  g_small_override (probes) wins when >= 0.
 int g_small_override = -1;
-constexpr unsigned SMALL_TILES_BELOW = 2;
 static int small_tiles_mode() {
     if (g_small_override >= 0) return g_small_override;
     static const int env = [] {
@@ -1472,12 +1471,16 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     const unsigned ntiles_all = (unsigned)(L.mtiles * L.ntiles) * nplanes * g.nsub;
     const unsigned ncu = device_cu_count();
     const int pmode = persistent_mode();
-    // small launches (fewer than SMALL_TILES_BELOW 256 x 256 tiles per CU): 128 x 128 tiles, two blocks per CU
-    // (gemm_i8_small_kernel).  GEMMUL8_SMALL_TILES=0 never, 1 wherever it applies (residue and bound products
-    // over buffer descriptors), unset by that rule unless GEMMUL8_PERSISTENT forces a 256-tile kernel.
+    // 128 x 128 tiles, two blocks per CU (gemm_i8_small_kernel): by default the accurate-mode bound product with
+    // fewer 256 x 256 tiles than CUs (1024^2: 16 tiles on 256 CUs; measured, profiles/r06/small_tiles/: the
+    // accurate scaling phase at 1024^3 63.7 -> 55.2 us, 1536^3 83.3 -> 73.3, 2048^3 100.6 -> 94.5).  Residue
+    // products only when forced: the 256-tile kernels are faster for them at every size measured (1024^3 22.7
+    // vs 29.5 us, 1536^3 55.1 vs 63.8, 2048^3 105 vs 130).  GEMMUL8_SMALL_TILES=0 never, 1 wherever it applies
+    // (residue and bound products over buffer descriptors), unset by that rule unless GEMMUL8_PERSISTENT forces
+    // a 256-tile kernel.
     const int smode = small_tiles_mode();
     if ((epi == Epi::RESIDUE || epi == Epi::BOUND) && buf &&
-        (smode == 1 || (smode == 2 && pmode == 2 && ntiles_all < SMALL_TILES_BELOW * ncu))) {
+        (smode == 1 || (smode == 2 && pmode == 2 && epi == Epi::BOUND && ntiles_all < ncu))) {
         const dim3 sgrid((unsigned)(4 * L.mtiles * L.ntiles), nplanes * g.nsub);
         if (epi == Epi::RESIDUE) {
             g_last_residue_kernel.store(4, std::memory_order_relaxed);

@@ -726,9 +726,9 @@ def test_persistent_default_matches_one_tile():
 
 
 def test_small_tiles_match_one_tile():
-    """The 128 x 128-tile product kernel (gemm_i8_small_kernel; the default below 2 tiles of 256 x 256 per CU):
-    C bit-identical to the 256-tile one-tile kernel (GEMMUL8_SMALL_TILES=0 GEMMUL8_PERSISTENT=0) and the rule's
-    default, child processes, at 1024^3 (224 tiles, the default rule), odd shapes with partial 128-tiles, k
+    """The 128 x 128-tile product kernel (gemm_i8_small_kernel; by default the accurate-mode bound product below
+    one 256 x 256 tile per CU): C bit-identical to the 256-tile one-tile kernel (GEMMUL8_SMALL_TILES=0
+    GEMMUL8_PERSISTENT=0) and the rule's default, child processes, at 1024^3, odd shapes with partial 128-tiles, k
     from 1 k-step to 33, accurate mode (the bound product runs the small kernel too), f32, Karatsuba complex
     sub-products, and with the kernel forced wherever it applies (GEMMUL8_SMALL_TILES=1: 2048^3, 3.5 tiles of
     256 x 256 per CU); the oracle checks the forced small kernel's slices, residues and C at small shapes"""
@@ -772,7 +772,8 @@ def test_small_tiles_match_one_tile():
             for name in ("default", "forced"):
                 assert np.array_equal(outs["onetile"][key].view(np.uint8), outs[name][key].view(np.uint8)), (name, key)
         assert str(outs["forced"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
-        assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
+        assert str(outs["forced"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
+        assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
         assert str(outs["default"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_persistent_kernel"
         assert str(outs["onetile"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
     code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
