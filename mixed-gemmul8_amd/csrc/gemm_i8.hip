@@ -330,26 +330,28 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I
                                          int wc, unsigned tm, unsigned tn, unsigned j, unsigned sb, bool active) {
     if constexpr (EPI == (int)Epi::RESIDUE || EPI == EPI_RESIDUE_ADD) {
         const int p = g.p[j];
-        uint32_t *lo = reinterpret_cast<uint32_t *>(smem);  // [256 cols][64 dwords], dword index ^= col & 31
-        // residues of the 4 x 2 fragments -> LDS, one fragment at a time (bounded VGPR use)
+        // residues -> LDS as [256 cols][PARK_CS dwords], dword d = rows 4d..4d+3 of the column.  The column stride of
+        // 68 dwords (272 B) keeps the 16-byte chunks aligned and spreads a 16 x 16 accumulator tile's dword writes
+        // over the banks (two lanes per bank), and every write of a lane is ONE base address plus an immediate
+        // offset (the XOR-swizzled layout before it cost ~5 address instructions per write and a runtime dword
+        // permutation per 16-byte read; tools/probes/onetile_ablate.hip)
+        constexpr int PARK_CS = 68;
+        static_assert(256 * PARK_CS * 4 <= LDS_BYTES, "park area");
+        uint32_t *lo = reinterpret_cast<uint32_t *>(smem);
+        uint32_t *pbase = lo + (wc * 64 + (lane & 15)) * PARK_CS + wr * 32 + (lane >> 4);
         auto park = [&](auto &&res) {
             if (!active) return;
 #pragma unroll
             for (int i = 0; i < ACC_I; ++i)
 #pragma unroll
                 for (int jj = 0; jj < ACC_J; ++jj) {
-                    const int col = wc * 64 + acc_col(jj, lane);
+                    uint32_t w = 0;
 #pragma unroll
-                    for (int gq = 0; gq < ACC_E / 4; ++gq) {  // four consecutive rows per dword
-                        uint32_t w = 0;
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][4 * gq + e]) << (8 * e);
-                        const int rdw = (wr * 128 + acc_row(i, 4 * gq, lane)) >> 2;
-                        lo[col * 64 + (rdw ^ (col & 31))] = w;
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
+                    for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][e]) << (8 * e);
+                    pbase[jj * 16 * PARK_CS + 4 * i] = w;
                 }
         };
+        static_assert(OZ2_MFMA16, "park map: 16x16 accumulator tiles");
         if (OZ2_ABLATE == 7 || (g.biased && p == 256)) {  // (7: probe) p = 256: bias is a multiple of 256
             park([&](int x) { return (uint32_t)x & 0xffu; });
         } else if (g.biased) {
@@ -369,12 +371,8 @@ __device__ __forceinline__ void epilogue(const GemmArgs &g, AccTile (&acc)[ACC_I
             if (tid >= 512) break;
             const int chunk = tid + 512 * it;
             const int col = chunk >> 4, qd = chunk & 15;
-            const int x = col & 31;
-            const uint4 v = *reinterpret_cast<const uint4 *>(lo + col * 64 + ((4 * qd) ^ (x & ~3)));
-            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
-            const int pm = x & 3;
+            uint4 res = *reinterpret_cast<const uint4 *>(lo + col * PARK_CS + 4 * qd);
             uint4 *dst = reinterpret_cast<uint4 *>(out + (size_t)col * g.ldo + 16 * qd);
-            uint4 res = make_uint4(e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]);
             if (OZ2_ABLATE == 9) {  // probe: no residue store
                 asm volatile("" ::"v"(res.x), "v"(res.y), "v"(res.z), "v"(res.w));
                 continue;
