@@ -1238,17 +1238,23 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
                     for (int jj = 0; jj < ACC_J; ++jj) asm volatile("" ::"v"(acc[i][jj]));
                 return;
             }
+            // dword 4 i + q of column col (rows 16 i + 4 q ..) at col * 32 + 4 (i ^ (col & 7)) + q: the 16-byte
+            // chunk i is XOR-swizzled by the column's low bits (two lanes per bank for a 16 x 16 tile's writes, no
+            // permutation inside a chunk), and col & 7 = lane & 7, so a lane's eight chunk positions are eight
+            // per-lane addresses computed once per tile, the four column blocks jj immediate offsets
+            const int t7 = elane & 7;
+            uint32_t *const pb = park + (wc * 64 + (elane & 15)) * 32 + (elane >> 4);
 #pragma unroll
-            for (int i = 0; i < ACC_I; ++i)
+            for (int i = 0; i < ACC_I; ++i) {
+                uint32_t *const pi = pb + 4 * (i ^ t7);
 #pragma unroll
                 for (int jj = 0; jj < ACC_J; ++jj) {
-                    const int col = wc * 64 + acc_col(jj, elane);
                     uint32_t w = 0;
 #pragma unroll
                     for (int e = 0; e < 4; ++e) w |= res(acc[i][jj][e]) << (8 * e);
-                    const int q = elane >> 4;  // dword 4 i + q of the column (rows 16 i + 4 q ..)
-                    park[col * 32 + ((i ^ ((col >> 1) & 7)) << 2) + (q ^ ((col & 1) << 1))] = w;
+                    pi[jj * 16 * 32] = w;
                 }
+            }
         };
         if (ABL == 1 || (g.biased && p == 256)) {
             park_all([&](int x) { return (uint32_t)x & 0xffu; });
@@ -1270,11 +1276,9 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
             if (ABL >= 2) break;
             const int chunk = gtid + 256 * it;
             const int col = chunk >> 3, c = chunk & 7;
-            const uint4 v = *reinterpret_cast<const uint4 *>(park + col * 32 + ((c ^ ((col >> 1) & 7)) << 2));
-            const int pm = (col & 1) << 1;
-            const uint32_t e[4] = {v.x, v.y, v.z, v.w};
+            const uint4 v = *reinterpret_cast<const uint4 *>(park + col * 32 + ((c ^ (col & 7)) << 2));
             typedef unsigned u4v __attribute__((ext_vector_type(4)));
-            const u4v val = u4v{e[0 ^ pm], e[1 ^ pm], e[2 ^ pm], e[3 ^ pm]};
+            const u4v val = u4v{v.x, v.y, v.z, v.w};
             u4v *dst = reinterpret_cast<u4v *>(out + (size_t)col * g.ldo + 16 * c);
             if (OZ2_RES_NTS) __builtin_nontemporal_store(val, dst);
             else *dst = val;
