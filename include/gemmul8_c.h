@@ -191,7 +191,8 @@ int gemmul8_set_epilogue(int mode);
 int gemmul8_get_epilogue(void);
 
 /* Name of the residue-product kernel the last products launch of this process took
- * ("gemm_i8_persistent_kernel", "gemm_i8_kernel", "gemm_i8_kernel (k-chunked)" or "none"). */
+ * ("gemm_i8_persistent_pg_kernel", "gemm_i8_persistent_kernel", "gemm_i8_kernel", "gemm_i8_small_kernel",
+ * "gemm_i8_kernel (k-chunked)" or "none"). */
 const char *gemmul8_last_products_kernel(void);
 
 /* --- bench / test harness (not part of the emulation path) ------------------------------------ */

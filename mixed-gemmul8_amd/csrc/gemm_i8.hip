@@ -1064,9 +1064,9 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
 #undef OZ2_STAMP
 }
 
-#ifdef OZ2_PG_PROBES
 // ---------------------------------------------------------------------------------------------
-// Persistent residue product with PER-GROUP epilogues (round 6).  The same DMA pipeline, tile queues and
+// Persistent residue product with PER-GROUP epilogues (round 6; the default, GEMMUL8_PG_EPILOGUE=0 selects
+// gemm_i8_persistent_kernel above).  The same DMA pipeline, tile queues and
 // main loop as gemm_i8_persistent_kernel, but the two wave groups (rows 0-127 / 128-255 of the tile) stay one
 // barrier apart for the whole launch: no realignment around the epilogue.  Each group parks and stores its
 // own 128 rows right after its own last MFMA interval, so per SIMD the intervals pair as
@@ -1075,8 +1075,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_kernel(GemmArg
 // (L = fragment reads + DMA issue, M = MFMAs; ' = the next tile): group 0's park runs beside group 1's last
 // MFMAs, and the two epilogues overlap each other instead of following each other with the whole block
 // waiting at four barriers.  Per tile each group passes 2K + 2 barriers.
-// MEASURED NEUTRAL (round 6, profiles/r06/epilogue_ab/): same residues, per-tile overhead within the run-to-run
-// spread of the block-epilogue kernel on three boxes; built into probe builds only (OZ2_PG_PROBES).
+// Measured in one process against the block-epilogue kernel (tools/probes/persist_pg_ab.hip, profiles/r06/epilogue_ab/):
+// with the park layout below, 0.5-1.2 % shorter at cfg2's shape and 2-5 % at k = 1024 (per-tile overhead 6.2-6.3
+// against 6.7-7.7 k-step equivalents, three runs on two boxes; the first layout, with XOR addresses per write and
+// a dword permutation per read-back, was neutral); identical residues.
 // Group 0 parks in the ring slot of the tile's last step (its next writer is group 0's own DMA of the next
 // tile's step 3, issued in L'(0) after its store sweep has read the slot back), group 1 in the spare 32 KiB.
 // The accumulators are not reset: the first MFMA of each tile reads its C operand from a splat of the
@@ -1292,8 +1294,6 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
     if (wr == 0) barrier();  // group 0 passed one barrier fewer (group 1's initial one)
 }
 
-#endif  // OZ2_PG_PROBES
-
 // Exhaustive check of the two residue epilogues against exact arithmetic, every input and every
 // modulus: path 0 = biased (x in [-2^30, 2^30], the accumulator starting at bias_i), path 1 = signed
 // Barrett (every int32, conv_32i_2_8u.hpp:7-56).  Counts mismatches into *count.
@@ -1379,12 +1379,18 @@ int g_prio_override = 1;  // probes: the persistent kernel's priority variant (P
 int g_epim_override = 0;  // probes: the persistent kernel's residue arithmetic (EPIM; 0 = the default)
 int g_order_override = 0;  // probes: the persistent kernel's k order (ORD; 0 = the default)
 unsigned long long *g_stamps = nullptr;  // probes: OZ2_STAMPS builds' per-wave phase sums
-#ifdef OZ2_PG_PROBES
-// probe builds: the persistent kernel's epilogue per wave group (gemm_i8_persistent_pg_kernel; g_pg_override 1,
-// ablations 2-4) or the default block epilogue (0)
-int g_pg_override = 0;
-static bool pg_epilogue() { return g_pg_override != 0; }
-#endif
+// the persistent kernel: per wave group epilogues (gemm_i8_persistent_pg_kernel, the default) or the block
+// epilogue (gemm_i8_persistent_kernel: GEMMUL8_PG_EPILOGUE=0, read once; A/B and the kernel the stamp / EPIM /
+// order probes instrument).  g_pg_override (probes) wins when >= 0; 2-4 are the per-group kernel's ablations.
+int g_pg_override = -1;
+static bool pg_epilogue() {
+    if (g_pg_override >= 0) return g_pg_override != 0;
+    static const bool env = [] {
+        const char *e = getenv("GEMMUL8_PG_EPILOGUE");
+        return e ? atoi(e) != 0 : true;
+    }();
+    return env;
+}
 // GEMMUL8_SMALL_TILES: 0 = never the 128 x 128 kernel, 1 = wherever it applies, unset (2) = the rule in
 // gemm_i8.  g_small_override (probes) wins when >= 0.
 int g_small_override = -1;
@@ -1506,16 +1512,19 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
             return e ? (unsigned)atoi(e) : 0u;
         }();
         const dim3 pgrid(std::min(std::min(ntiles_all, ncu), grid_cap ? std::max(grid_cap, 8u) : ncu));
+        // (the probe overrides below select the block-epilogue kernel's variants)
+        const bool probe_variant = g_epim_override != 0 || g_prio_override != 1 || g_order_override != 0;
+        if (pg_epilogue() && !probe_variant) {
 #ifdef OZ2_PG_PROBES
-        if (pg_epilogue()) {
             if (g_pg_override == 2) launch(gemm_i8_persistent_pg_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
             else if (g_pg_override == 3) launch(gemm_i8_persistent_pg_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
             else if (g_pg_override == 4) launch(gemm_i8_persistent_pg_kernel<false, 1, 3>, pgrid, dim3(NTHREADS), st, g);
-            else if (g.nsub == 3) launch(gemm_i8_persistent_pg_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
-            else launch(gemm_i8_persistent_pg_kernel<false, 1>, pgrid, dim3(NTHREADS), st, g);
-        } else
+            else
 #endif
-        if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
+            if (g.nsub == 3) launch(gemm_i8_persistent_pg_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
+            else launch(gemm_i8_persistent_pg_kernel<false, 1>, pgrid, dim3(NTHREADS), st, g);
+            g_last_residue_kernel.store(5, std::memory_order_relaxed);
+        } else if (g.nsub == 3) launch(gemm_i8_persistent_kernel<true, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 1) launch(gemm_i8_persistent_kernel<false, 1, 1>, pgrid, dim3(NTHREADS), st, g);
         else if (g_epim_override == 2) launch(gemm_i8_persistent_kernel<false, 1, 2>, pgrid, dim3(NTHREADS), st, g);
 #ifdef OZ2_EPIM_PROBES

@@ -822,6 +822,7 @@ const char *gemmul8_last_products_kernel(void) {
     case 2: return "gemm_i8_persistent_kernel";
     case 3: return "gemm_i8_kernel (k-chunked)";
     case 4: return "gemm_i8_small_kernel";
+    case 5: return "gemm_i8_persistent_pg_kernel";
     default: return "none";
     }
 }

@@ -681,11 +681,13 @@ def test_persistent_products_forced():
             "print('OK')")
     tdir = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(tdir)
-    for cap in ("", "16"):
-        env = dict(os.environ, GEMMUL8_PERSISTENT="1", GEMMUL8_PERSISTENT_GRID=cap, GEMMUL8_CPLX_PRODUCTS="karatsuba")
+    # the per-group-epilogue kernel (default) with and without a capped grid, and the block-epilogue kernel
+    for cap, pg in (("", "1"), ("16", "1"), ("16", "0")):
+        env = dict(os.environ, GEMMUL8_PERSISTENT="1", GEMMUL8_PERSISTENT_GRID=cap, GEMMUL8_CPLX_PRODUCTS="karatsuba",
+                   GEMMUL8_PG_EPILOGUE=pg)
         r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")], env=env,
                            capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0 and "OK" in r.stdout, (cap, r.stderr[-3000:])
+        assert r.returncode == 0 and "OK" in r.stdout, (cap, pg, r.stderr[-3000:])
 
 
 def test_persistent_default_matches_one_tile():
@@ -774,7 +776,7 @@ def test_small_tiles_match_one_tile():
         assert str(outs["forced"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
         assert str(outs["forced"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
         assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
-        assert str(outs["default"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_persistent_kernel"
+        assert str(outs["default"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_persistent_pg_kernel"
         assert str(outs["onetile"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
     code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
             "from test_gpu_parity import check_full\nfrom util import randmat_np\n"

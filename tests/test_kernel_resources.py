@@ -17,8 +17,9 @@ pytestmark = pytest.mark.skipif(not shutil.which("llvm-readelf", path="/opt/rocm
 
 # demangled-name prefix -> minimum waves per SIMD
 FLOORS = {
-    "oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>": 2,  # cfg2/3/4 products: 512 threads, 160 KiB LDS, 1 block per CU
-    "oz2::gemm_i8_persistent_kernel<true, 1, 0, 0>": 2,  # cfg5 (Karatsuba sub-products)
+    "oz2::gemm_i8_persistent_pg_kernel<false, 1, 0>": 2,  # cfg2/3/4 products: 512 threads, 160 KiB LDS, 1 block per CU
+    "oz2::gemm_i8_persistent_pg_kernel<true, 1, 0>": 2,   # cfg5 (Karatsuba sub-products)
+    "oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>": 2,  # the block-epilogue form (GEMMUL8_PG_EPILOGUE=0)
     "oz2::gemm_i8_small_kernel<0, false>": 2,       # small launches: 256 threads, 64 KiB LDS, 2 blocks per CU
     "oz2::gemm_i8_small_kernel<1, false>": 2,       # the accurate-mode bound product of small problems
     "oz2::crt_kernel<0, false, 14u, false, 8>": 5,     # cfg2/3 CRT
@@ -66,8 +67,9 @@ def test_hot_kernel_occupancy(table, prefix):
 
 
 @pytest.mark.parametrize("prefix,loads,stores", [
-    ("oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>(", 0, 8),  # residue stores (LDS-DMA loads are buffer ops)
-    ("oz2::gemm_i8_persistent_kernel<true, 1, 0, 0>(", 0, 8),
+    ("oz2::gemm_i8_persistent_pg_kernel<false, 1, 0>(", 0, 8),  # residue stores (LDS-DMA loads are buffer ops)
+    ("oz2::gemm_i8_persistent_pg_kernel<true, 1, 0>(", 0, 8),
+    ("oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>(", 0, 8),
     ("oz2::crt_kernel<0, false, 14u, false, 8>(", 14, 4),     # 14 residue planes, C stored in 16-byte vectors
     ("oz2::crt_kernel<2, false, 12u, true, 8>(", 36, 8),      # 3 Karatsuba sub-planes x 12 moduli
 ])

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of whole library builds: python tools/probes/lib_ab.py <variant dir> [<variant dir> ...]
-Each directory holds a gemmul8/ package with its own libgemmul8_amd.so.  Every variant runs in its own
+"""A/B of whole library builds: python tools/probes/lib_ab.py <variant> [<variant> ...]
+A variant is a directory holding a gemmul8/ package with its own libgemmul8_amd.so, optionally followed by
+@NAME=VALUE,... environment settings for its process (one library, two settings: dir@GEMMUL8_X=0 dir@GEMMUL8_X=1).  Every variant runs in its own
 subprocess, alternating over LIB_AB_ROUNDS (default 2) rounds: cfg2 (8192^3, N = 14), cfg5 (complex 4096^3, N = 12, Karatsuba
 products) and 8192^2 x 1024 (16 k-steps per tile: the epilogue's share is large), 20 timed calls each after
 3 warm-ups; prints ms per call, the phase times (scaling, products, CRT) and a hash of C (the variants must
@@ -48,7 +49,10 @@ def main():
     res = {}
     for rnd in range(int(os.environ.get("LIB_AB_ROUNDS", "2"))):
         for v in sys.argv[1:]:
-            r = subprocess.run([sys.executable, "-c", CHILD, v], capture_output=True, text=True, timeout=300)
+            # "dir" or "dir@NAME=VALUE,NAME=VALUE": the variant's library, with environment settings of its own
+            path, _, envs = v.partition("@")
+            env = dict(os.environ, **dict(x.split("=", 1) for x in envs.split(",") if x))
+            r = subprocess.run([sys.executable, "-c", CHILD, path], capture_output=True, text=True, timeout=300, env=env)
             if r.returncode != 0:
                 print(v, "failed", r.stderr[-2000:])
                 sys.exit(1)

@@ -42,6 +42,7 @@ int main(int argc, char **argv) {
     fill_rand<<<4096, 256>>>((uint32_t *)w, total / 4, 12345u);
     oz2::ModParams MP = oz2::make_mod_params(N);
     oz2::g_persistent_override = 1;
+    oz2::g_pg_override = 0;  // the block-epilogue kernel (this probe instruments it)
     std::vector<float> t[NK];
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);

@@ -39,6 +39,7 @@ int main(int argc, char **argv) {
     if (hipMalloc(&st, nst * 8) != hipSuccess) return 1;
     (void)hipMemset(st, 0, nst * 8);
     oz2::g_persistent_override = 1;
+    oz2::g_pg_override = 0;  // the block-epilogue kernel (this probe instruments it)
     uint32_t *queue = reinterpret_cast<uint32_t *>(b + L.offQueue);
     for (int rep = 0; rep < 4; ++rep) {
         oz2::g_stamps = rep == 3 ? st : nullptr;  // the last launch records
