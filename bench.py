@@ -4,8 +4,11 @@
 Workloads (BASELINE.json configs):
   cfg2 (default at --gpus 1)  DGEMM emulation m = n = k = 8192, num_moduli = 14, fast mode, 1 GPU
   cfg3 (default at --gpus N>1) DGEMM emulation m = n = k = 16384, num_moduli = 14, fast mode, the
-                               (modulus, column block) units sharded over N GPUs (gemmul8.dist.gemm_moduli):
-                               strong scaling of ONE product, C left distributed by column blocks
+                               (modulus, column block) units sharded over N GPUs: strong scaling of ONE product,
+                               C left distributed.  --partition auto (default): at an even N >= 4 the 2-D unit
+                               grid (gemmul8.dist.gemm_moduli_grid: 2 row blocks, each a (modulus, column block)
+                               partition of its rows over N / 2 ranks), else gemmul8.dist.gemm_moduli over all N;
+                               the other one is timed among the variants
   cfg4                         mixed FP64 * FP32 -> FP64, 8192^3, num_moduli = 10, accurate mode, 1 GPU
   cfg5                         complex DGEMM (COMPLEX_BIG_MATRIX_ENCODE), 4096^3, num_moduli = 12, 1 GPU
 Inputs come from the reference driver's generator (hiprand XORWOW, (U - 0.5) * exp(0.5 * N(0,1)),
@@ -62,7 +65,9 @@ def parse(argv=None):
     ap.add_argument("--size", type=int, default=None, help="override m = n = k")
     ap.add_argument("--moduli", type=int, default=None)
     ap.add_argument("--accurate", action="store_true")
-    ap.add_argument("--partition", choices=["moduli", "rows"], default="moduli")
+    ap.add_argument("--partition", choices=["auto", "moduli", "grid", "rows"], default="auto",
+                    help="multi-GPU: auto = grid (gemm_moduli_grid, 2 row blocks) for fast mode on an even W >= 4 whose "
+                         "sub-groups exist, else moduli (gemm_moduli); rows = the weak-scaling row partition")
     ap.add_argument("--order", choices=["moduli", "columns"], default="moduli",
                     help="moduli partition: unit order of gemmul8.dist.ShardPlan")
     ap.add_argument("--gather", action="store_true", help="moduli partition: collect C on rank 0 in the step")
@@ -410,6 +415,8 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lam
         v = reduce_max(time.perf_counter() - t0, world) / steps * 1e3
         put(out, name, {"ms_per_step": round(v, 3), "tflops": round(flops / (v * 1e-3) / 1e12, 1)})
 
+    timed("moduli_columns",  # gemm_moduli over all W ranks, C distributed (the headline where the grid is not)
+        lambda: GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, ops=ops, order=args.order))
     timed("moduli_columns_gathered",
         lambda: GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, torch.float64, gather=True, ops=ops))
     timed("moduli_whole_planes_to_root",
@@ -461,13 +468,41 @@ def time_variants(G, GD, A, B, m, n, k, N, fast, world, rank, args, ops, arm=lam
 def select_workload(args, world):
     """the configuration this run measures: --workload, else cfg2 on one GPU and cfg3 (the moduli-sharded
     BASELINE config) on more; --size / --moduli / --accurate make it a custom one"""
-    name = args.workload or ("cfg3" if (world > 1 and args.partition == "moduli") else "cfg2")
+    name = args.workload or ("cfg3" if (world > 1 and args.partition != "rows") else "cfg2")
     wl = WORKLOADS[name]
     m = args.size or wl["size"]
     N = args.moduli or wl["moduli"]
     fast = not (args.accurate or wl["accurate"])
     custom = m != wl["size"] or N != wl["moduli"] or fast == wl["accurate"]
     return {"name": name, "wl": wl, "m": m, "N": N, "fast": fast, "kind": wl["kind"], "custom": custom}
+
+
+def source_sha16():
+    """the first 16 hex digits of the sha256 of the host sources that decide a line (bench.py, gemmul8/dist.py,
+    gemmul8/__init__.py): a committed line can be checked against the revision under test"""
+    out = {}
+    for rel in ("bench.py", "mixed-gemmul8_amd/gemmul8/dist.py", "mixed-gemmul8_amd/gemmul8/__init__.py"):
+        try:
+            with open(os.path.join(ROOT, rel), "rb") as f:
+                out[os.path.basename(rel) if rel != "mixed-gemmul8_amd/gemmul8/__init__.py" else "gemmul8/__init__.py"] = \
+                    hashlib.sha256(f.read()).hexdigest()[:16]
+        except OSError:
+            pass
+    return out
+
+
+def resolve_partition(args, world, fast):
+    """the partition of a multi-GPU run: --partition, or for auto the 2-D unit grid (gemm_moduli_grid: 2 row blocks
+    of W / 2 ranks, each a (modulus, column block) partition of its rows) where it applies -- fast mode, an even
+    W >= 4, sub-groups created at setup -- else the (modulus, column block) units over all W ranks.  The grid is
+    the headline because the cfg3 per-rank replay measured it faster by more than the run-to-run spread
+    (profiles/r06/cfg3_partitions/: slowest rank 6.070 / 6.063 ms against 6.194 / 6.179 ms, one box)"""
+    if world <= 1:
+        return "single"
+    if args.partition != "auto":
+        return args.partition
+    grid_ok = fast and world >= 4 and world % 2 == 0 and os.environ.get("GEMMUL8_BENCH_NO_GRID") is None
+    return "grid" if grid_ok else "moduli"
 
 
 def labels(W):
@@ -547,21 +582,34 @@ def main():
     ct = G.COMPLEX_BIG_MATRIX_ENCODE if cplx else G.REAL_DEFAULT
     flop_per = (8.0 if cplx else 2.0) * m * n * k
     dev = torch.device("cuda", torch.cuda.current_device())
-    sharded = world > 1 and args.partition == "moduli"
+    part = resolve_partition(args, world, fast)
+    sharded = part in ("moduli", "grid")
+    grid = part == "grid"
     rows_accurate = world > 1 and not sharded and not fast
     seed = 123456 + (rank if (world > 1 and not sharded) else 0)
     arm("setup")
     A, B, tc = make_operands(kind, m, n, k, seed, dev)
     L = G.layout(m, n, k, N, ct)
     trace = None
+    # the rows [r0, r1) of C this rank's units cover and its index in the plan (grid: its row block's sub-plan)
+    r0, r1, prank = 0, m, rank
+    if grid:
+        Gs = world // 2
+        hblk, prank = divmod(rank, Gs)
+        r0, r1 = GD.blocks(m, 2)[hblk]
     if sharded:
         ops = GD.HipShardOps()
-        plan = GD.ShardPlan(m, n, N, world, order=args.order)
+        plan = GD.ShardPlan(r1 - r0, n, N, world // 2 if grid else world, order=args.order)
         trace = []
 
-        def step(tr=None):
-            return GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, tc, ct, gather=args.gather, ops=ops,
-                                  trace=tr, order=args.order)
+        if grid:
+            def step(tr=None):
+                return GD.gemm_moduli_grid(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, tc, ct, row_blocks=2,
+                                           gather=args.gather, ops=ops, order=args.order, trace=tr)
+        else:
+            def step(tr=None):
+                return GD.gemm_moduli(G.OP_N, G.OP_N, m, n, k, A, m, B, k, N, fast, tc, ct, gather=args.gather,
+                                      ops=ops, trace=tr, order=args.order)
     elif rows_accurate:
         # accurate row blocks: B's column shifts come from the bound product over ALL rows of A, so the ranks
         # MAX-combine its column maxima (gemmul8.dist.matmul_rows); row-major operands: op T on both
@@ -613,15 +661,15 @@ def main():
     work_alg = algorithmic_work(m, n, k, N, kind, fast, L)
     if sharded:
         # dominant kernel: the int8 products of rank 0's units (one products_cols launch per merged unit)
-        ops_step = sum(2.0 * m * (c1 - c0) * k * fmac * (j1 - j0) for j0, j1, c0, c1 in plan.launches[rank])
-        planes = sum((c1 - c0) * (j1 - j0) for j0, j1, c0, c1 in plan.launches[rank]) / n
+        ops_step = sum(2.0 * (r1 - r0) * (c1 - c0) * k * fmac * (j1 - j0) for j0, j1, c0, c1 in plan.launches[prank])
+        planes = sum((c1 - c0) * (j1 - j0) for j0, j1, c0, c1 in plan.launches[prank]) / n
         seg = {}
         for i in range(0, len(trace), 6):
             evs = trace[i:i + 6]
             for (a, ea), (b, eb) in zip(evs, evs[1:]):
                 seg[b] = seg.get(b, 0.0) + ea.elapsed_time(eb)
         extra["step_phases_ms_rank0"] = {kk: round(v / args.steps, 4) for kk, v in seg.items()}
-        extra["launches_rank0"] = [list(u) for u in plan.launches[rank]]
+        extra["launches_rank0"] = [list(u) for u in plan.launches[prank]]
     else:
         ops_step = 2.0 * fmac * m * n * k * N
         planes = N
@@ -671,13 +719,16 @@ def main():
             "data": "synthetic: hiprand XORWOW (U-0.5)*exp(0.5*N(0,1)), seed 123456, A == B as in the reference "
                     "driver" + (" (row partition: rank r's A seed 123456+r)" if (world > 1 and not sharded) else ""),
             "config": {"workload": workload, "m": m, "n": n, "k": k, "num_moduli": N, "fastmode": fast,
-                       "parallelism": (("moduli x column blocks" if sharded else "rows") + f" x{world}")
+                       "parallelism": ((f"row blocks 2 x (moduli x column blocks) x{world // 2}" if grid else
+                                        "moduli x column blocks" if sharded else "rows") + f" x{world}")
                        if world > 1 else "single",
+                       "partition": part,
                        "world_size": world, "backend": backend or "none",
                        "output": ("C gathered on rank 0" if args.gather else "C distributed by column blocks")
                        if sharded else "C on each rank"},
             "roofline": roofline,
             "cpu_baseline": report["cpu"],
+            "source_sha16": source_sha16(),
         }
 
         if sharded:
@@ -709,11 +760,12 @@ def main():
         Cout = step()
         torch.cuda.synchronize()
         if sharded:
-            c0, c1 = plan.cols[rank]
+            c0, c1 = plan.cols[prank]
             if args.gather:
-                Cout = None if rank else Cout[c0:c1]
-            if c1 > c0 and Cout is not None:
-                C1, C2 = G.dd_gemm(A, B[c0:c1], m, c1 - c0, k)
+                Cout = None if rank else Cout[c0:c1, r0:r1]
+            if c1 > c0 and r1 > r0 and Cout is not None:
+                Ab = A if not grid else A[:, r0:r1].contiguous()  # (the rows of this rank's row block)
+                C1, C2 = G.dd_gemm(Ab, B[c0:c1], r1 - r0, c1 - c0, k)
                 emax, emed = G.relerr_dd(Cout, C1, C2)
                 del C1, C2
             else:

@@ -705,7 +705,7 @@ def release_grid_groups():
 
 def gemm_moduli_grid(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=True, out_dtype=None,
                      computeType=REAL_DEFAULT, group=None, row_blocks=2, gather=False, root=0, ops=None,
-                     align=TILE, order="moduli"):
+                     align=TILE, order="moduli", trace=None):
     """The 2-D unit grid (moduli x row blocks x column blocks): the W ranks form H row blocks of G = W / H ranks;
     the ranks of row block h run gemm_moduli on its rows of op(A) (rows blocks(m, H)[h], B replicated) over their
     own sub-group, i.e. (modulus, column block) units of that row block and the residue exchange among those G
@@ -717,7 +717,8 @@ def gemm_moduli_grid(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=
 
     Returns this rank's block -- rows blocks(m, H)[h], columns ShardPlan(m_h, n, N, G).cols[rank % G] -- as a
     (c1 - c0, m_h) tensor (column-major), or with gather=True the whole (n, m) C on the root and None
-    elsewhere.  A, B: column-major storage as in gemm_moduli (op N: an (k, m) tensor; op T: an (m, k) one)."""
+    elsewhere.  A, B: column-major storage as in gemm_moduli (op N: an (k, m) tensor; op T: an (m, k) one).
+    trace: as gemm_moduli's, for this rank's row-block call."""
     if not fastmode:
         raise ValueError("gemm_moduli_grid: fast mode only (accurate-mode column shifts span every row block)")
     rank, world = _group_info(group)
@@ -737,7 +738,7 @@ def gemm_moduli_grid(opA, opB, m, n, k, A, lda, B, ldb, num_moduli=14, fastmode=
     mh = r1 - r0
     if mh > 0:
         Cb = gemm_moduli(opA, opB, mh, n, k, Ah, lda, B, ldb, num_moduli, fastmode, out_dtype, computeType,
-                         group=subgroups[h], gather=gather, root=0, ops=ops, align=align, order=order)
+                         group=subgroups[h], gather=gather, root=0, ops=ops, align=align, trace=trace, order=order)
     elif gather:  # (every rank of an empty row block skips, so its sub-group stays consistent)
         Cb = torch.empty((n, 0), dtype=out_dtype, device=A.device) if sub == 0 else None
     else:

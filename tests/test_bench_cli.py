@@ -51,6 +51,25 @@ def test_workload_selection_and_labels():
     assert (W["m"], W["N"], W["kind"]) == (4096, 12, "z") and "ZGEMM" in b.labels(W)[1]
 
 
+def test_headline_partition(monkeypatch):
+    """--partition auto: the 2-D unit grid at an even W >= 4 in fast mode (measured faster than the moduli units on
+    the cfg3 replay, profiles/r06/cfg3_partitions/), the (modulus, column block) units otherwise; an explicit
+    --partition wins; sub-groups that failed at setup (GEMMUL8_BENCH_NO_GRID) fall back to moduli"""
+    b = _bench()
+    monkeypatch.delenv("GEMMUL8_BENCH_NO_GRID", raising=False)
+    assert b.resolve_partition(b.parse(["--gpus", "8"]), 8, True) == "grid"
+    assert b.resolve_partition(b.parse(["--gpus", "4"]), 4, True) == "grid"
+    assert b.resolve_partition(b.parse(["--gpus", "2"]), 2, True) == "moduli"
+    assert b.resolve_partition(b.parse(["--gpus", "6"]), 6, True) == "grid"
+    assert b.resolve_partition(b.parse(["--gpus", "8", "--accurate"]), 8, False) == "moduli"
+    assert b.resolve_partition(b.parse(["--gpus", "8", "--partition", "moduli"]), 8, True) == "moduli"
+    assert b.resolve_partition(b.parse(["--gpus", "8", "--partition", "rows"]), 8, True) == "rows"
+    assert b.resolve_partition(b.parse([]), 1, True) == "single"
+    monkeypatch.setenv("GEMMUL8_BENCH_NO_GRID", "1")
+    assert b.resolve_partition(b.parse(["--gpus", "8"]), 8, True) == "moduli"
+    assert b.select_workload(b.parse(["--gpus", "8"]), 8)["name"] == "cfg3"
+
+
 def test_algorithmic_work_and_composite_roofline():
     """cfg2's fused-minimum bytes (operands once, slices and residues written and read once,
     C once) and the composite fraction; the per-phase GB/s follow from phase_ms"""
