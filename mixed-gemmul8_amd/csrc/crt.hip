@@ -377,7 +377,7 @@ template <typename E, int R = CRT_ROWS> __device__ __forceinline__ int crt_slot(
     return l * R + (e ^ ((EPV * (l >> SH)) & (R - 1)));
 }
 
-template <int OT, bool NUMM1, unsigned N, bool KARA = false, int R = CRT_ROWS>
+template <int OT, bool NUMM1, unsigned N, bool KARA = false, int R = CRT_ROWS, bool PFC = false>
 __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     static_assert(R == CRT_ROWS || KARA, "rows per lane other than CRT_ROWS: Karatsuba form only");
     using W = RowWord<R>;
@@ -396,11 +396,24 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
 #pragma unroll
     for (int e = 0; e < R; ++e) sa[e] = e < nr ? a.sftA[r0 + e] : 0;
     E *wb = buf[wv];
+    // real outputs with several columns per block (PF): the next column's residue words are loaded before this
+    // column's CRT, so they are in flight under its arithmetic and stores
+    constexpr bool PF = PFC && !KARA && OT < 2;
+    W wpf[PF ? N : 1];
+    if constexpr (PF) {
+        if (nr > 0 && blockIdx.y < a.n) load_rows<N>(a, blockIdx.y * a.ldr + r0, nr == R, nr, wpf);
+    }
     for (size_t col = blockIdx.y; col < a.n; col += gridDim.y) {
         const int sB = a.sftB[col];
         if (nr > 0) {
             W w[N], wi[N];
             const size_t off = col * a.ldr + r0;
+            if constexpr (PF) {
+#pragma unroll
+                for (unsigned i = 0; i < N; ++i) w[i] = wpf[i];
+                const size_t nxt = col + gridDim.y;
+                if (nxt < a.n) load_rows<N>(a, nxt * a.ldr + r0, nr == R, nr, wpf);
+            }
             if constexpr (KARA) {
                 // real parts from P1, P2 first, then the imaginary parts with P3: two sub-planes' words
                 // live at a time instead of three (occupancy; the residues are the same bytes)
@@ -458,7 +471,7 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
                         else wb[crt_slot<E, R>(lane, e)].y = __double2float_rn(vi);
                     }
                 }
-            } else {
+            } else if constexpr (!PF) {
                 load_rows<N>(a, off, nr == R, nr, w);
                 if (OT >= 2) load_rows<N>(a, off + a.imag_off, nr == R && (a.imag_off & 7) == 0, nr, wi);
             }
@@ -542,7 +555,8 @@ template <int OT, bool NUMM1, unsigned N, bool KARA>
 static void launch_crt_n(const CrtArgs &a, dim3 grid, hipStream_t st) {
     constexpr int R = KARA ? OZ2_KARA_ROWS : CRT_ROWS;
     grid.x = (unsigned)((a.m + 256 * R - 1) / (256 * R));
-    launch(crt_kernel<OT, NUMM1, N, KARA, R>, grid, dim3(256), st, a);
+    if (!KARA && OT < 2 && grid.y < a.n) launch(crt_kernel<OT, NUMM1, N, KARA, R, true>, grid, dim3(256), st, a);
+    else launch(crt_kernel<OT, NUMM1, N, KARA, R>, grid, dim3(256), st, a);
 }
 
 template <int OT, bool NUMM1, bool KARA = false>
@@ -584,7 +598,16 @@ void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const i
         break;
     }
     const unsigned gx = (unsigned)((L.m + 256 * CRT_ROWS - 1) / (256 * CRT_ROWS));
-    const unsigned gy = (unsigned)(L.n < 65535 ? L.n : 65535);
+    // columns per block of the real CRT (GEMMUL8_CRT_COLS, read once; A/B): the next column's residues are
+    // prefetched under the current one's arithmetic (crt_kernel, PF)
+    static const unsigned cols_per_block = [] {
+        const char *e = getenv("GEMMUL8_CRT_COLS");
+        const int v = e ? atoi(e) : 1;
+        return (unsigned)(v >= 1 && v <= 64 ? v : 1);
+    }();
+    const unsigned cpb = (ot == OutType::F64 || ot == OutType::F32) ? cols_per_block : 1u;
+    const size_t gyn = (L.n + cpb - 1) / cpb;
+    const unsigned gy = (unsigned)(gyn < 65535 ? gyn : 65535);
     dim3 grid(gx, gy);
     const bool nm1 = CP.numM1 != 0;
     switch (ot) {

@@ -22,9 +22,9 @@ FLOORS = {
     "oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>": 2,  # the block-epilogue form (GEMMUL8_PG_EPILOGUE=0)
     "oz2::gemm_i8_small_kernel<0, false>": 2,       # small launches: 256 threads, 64 KiB LDS, 2 blocks per CU
     "oz2::gemm_i8_small_kernel<1, false>": 2,       # the accurate-mode bound product of small problems
-    "oz2::crt_kernel<0, false, 14u, false, 8>": 5,     # cfg2/3 CRT
-    "oz2::crt_kernel<0, false, 10u, false, 8>": 5,     # cfg4 CRT
-    "oz2::crt_kernel<2, false, 12u, true, 8>": 3,      # cfg5 CRT (Karatsuba residues)
+    "oz2::crt_kernel<0, false, 14u, false, 8, false>": 5,    # cfg2/3 CRT
+    "oz2::crt_kernel<0, false, 10u, false, 8, false>": 5,    # cfg4 CRT
+    "oz2::crt_kernel<2, false, 12u, true, 8, false>": 3,     # cfg5 CRT (Karatsuba residues)
     "oz2::stats_pair_kernel<16, true>": 8,             # cfg2 shifts
     "oz2::encode_pair_kernel<double, false, false, true, true>": 4,  # cfg2 slices
     "oz2::encode_kernel<double, true, false, false, 0, true>": 2,    # cfg5 slices
@@ -70,8 +70,8 @@ def test_hot_kernel_occupancy(table, prefix):
     ("oz2::gemm_i8_persistent_pg_kernel<false, 1, 0>(", 0, 8),  # residue stores (LDS-DMA loads are buffer ops)
     ("oz2::gemm_i8_persistent_pg_kernel<true, 1, 0>(", 0, 8),
     ("oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>(", 0, 8),
-    ("oz2::crt_kernel<0, false, 14u, false, 8>(", 14, 4),     # 14 residue planes, C stored in 16-byte vectors
-    ("oz2::crt_kernel<2, false, 12u, true, 8>(", 36, 8),      # 3 Karatsuba sub-planes x 12 moduli
+    ("oz2::crt_kernel<0, false, 14u, false, 8, false>(", 14, 4),     # 14 residue planes, C stored in 16-byte vectors
+    ("oz2::crt_kernel<2, false, 12u, true, 8, false>(", 36, 8),      # 3 Karatsuba sub-planes x 12 moduli
 ])
 def test_streaming_memory_ops(prefix, loads, stores):
     """the streams read or written once per call stay out of the caches (non-temporal), and the
