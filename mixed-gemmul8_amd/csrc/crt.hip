@@ -598,14 +598,15 @@ void crt_inverse(const uint8_t *R, const Layout &L, const int16_t *sftA, const i
         break;
     }
     const unsigned gx = (unsigned)((L.m + 256 * CRT_ROWS - 1) / (256 * CRT_ROWS));
-    // columns per block of the real CRT (GEMMUL8_CRT_COLS, read once; A/B): the next column's residues are
-    // prefetched under the current one's arithmetic (crt_kernel, PF)
-    static const unsigned cols_per_block = [] {
+    // columns per block of the real CRT: the next column's residues are prefetched under the current one's
+    // arithmetic (crt_kernel, PF).  4 from n = 4096 (cfg2 CRT 0.2622 -> 0.2593 ms, 8192^2 x 1024 0.2679 ->
+    // 0.2651 ms, three interleaved rounds, same bits: profiles/r06/crt_cols/); GEMMUL8_CRT_COLS (read once) forces it
+    static const int cols_forced = [] {
         const char *e = getenv("GEMMUL8_CRT_COLS");
-        const int v = e ? atoi(e) : 1;
-        return (unsigned)(v >= 1 && v <= 64 ? v : 1);
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 64 ? v : 0;
     }();
-    const unsigned cpb = (ot == OutType::F64 || ot == OutType::F32) ? cols_per_block : 1u;
+    const unsigned cpb = (ot == OutType::F64 || ot == OutType::F32) ? (cols_forced ? (unsigned)cols_forced : L.n >= 4096 ? 4u : 1u) : 1u;
     const size_t gyn = (L.n + cpb - 1) / cpb;
     const unsigned gy = (unsigned)(gyn < 65535 ? gyn : 65535);
     dim3 grid(gx, gy);

@@ -22,7 +22,8 @@ FLOORS = {
     "oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>": 2,  # the block-epilogue form (GEMMUL8_PG_EPILOGUE=0)
     "oz2::gemm_i8_small_kernel<0, false>": 2,       # small launches: 256 threads, 64 KiB LDS, 2 blocks per CU
     "oz2::gemm_i8_small_kernel<1, false>": 2,       # the accurate-mode bound product of small problems
-    "oz2::crt_kernel<0, false, 14u, false, 8, false>": 5,    # cfg2/3 CRT
+    "oz2::crt_kernel<0, false, 14u, false, 8, false>": 5,    # cfg2/3 CRT below n = 4096
+    "oz2::crt_kernel<0, false, 14u, false, 8, true>": 4,     # cfg2/3 CRT (4 columns per block, prefetch)
     "oz2::crt_kernel<0, false, 10u, false, 8, false>": 5,    # cfg4 CRT
     "oz2::crt_kernel<2, false, 12u, true, 8, false>": 3,     # cfg5 CRT (Karatsuba residues)
     "oz2::stats_pair_kernel<16, true>": 8,             # cfg2 shifts
