@@ -686,7 +686,9 @@ def grid_groups(world, row_blocks, group=None):
     # destroy_process_group is torn down at interpreter exit, where gloo's threads abort the process
     wgroup = getattr(getattr(dist, "group", None), "WORLD", None)
     base = group if group is not None else wgroup
-    key = (id(base), world, row_blocks)
+    # (the global rank is part of the key only for ranks simulated as threads of one process, tests/fake_nccl.py:
+    # every rank must enter the creation itself)
+    key = (id(base), world, row_blocks, dist.get_rank())
     hit = _GRID_GROUPS.get(key)
     if hit is None or hit[0]() is not base:
         G = world // row_blocks

@@ -20,11 +20,14 @@ __global__ __launch_bounds__(256) void copy_pattern(const uint8_t *R, size_t pla
         uint64_t x = 0;
 #pragma unroll
         for (unsigned i = 0; i < N; ++i) x ^= w[i];
+        // C stores as the CRT issues them after its LDS transpose: 16 bytes per lane, lanes adjacent (the wave's
+        // 512 rows = 4 KiB of the column in four 1 KiB store instructions)
         typedef int i4v __attribute__((ext_vector_type(4)));
         i4v v = {(int)x, (int)(x >> 32), (int)x, (int)(x >> 32)};
-        i4v *dst = reinterpret_cast<i4v *>(C + col * ldc + r0);
+        const int lane = threadIdx.x & 63;
+        i4v *dst = reinterpret_cast<i4v *>(C + col * ldc + (r0 - (size_t)lane * 8));
 #pragma unroll
-        for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(v, dst + q);
+        for (int q = 0; q < 4; ++q) __builtin_nontemporal_store(v, dst + q * 64 + lane);
     }
 }
 
