@@ -379,7 +379,7 @@ template <typename E, int R = CRT_ROWS> __device__ __forceinline__ int crt_slot(
 
 template <int OT, bool NUMM1, unsigned N, bool KARA = false, int R = CRT_ROWS, bool PFC = false>
 __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
-    static_assert(R == CRT_ROWS || KARA, "rows per lane other than CRT_ROWS: Karatsuba form only");
+    static_assert(R == CRT_ROWS || R == 4, "rows per lane: 8 or 4");
     using W = RowWord<R>;
     using E = typename OutElem<OT>::T;
     constexpr int EPV = 16 / sizeof(E);  // elements per 16-byte vector
@@ -551,12 +551,33 @@ __global__ __launch_bounds__(256) void crt_kernel(CrtArgs a) {
     }
 }
 
+// rows per lane of the real CRT: 4 (twice the waves of 8; every wave of a block busy at m = 1024; measured
+// faster at every size) without the next-column prefetch (it costs 8% at cfg2 with 4 rows; it pays with
+// 8); GEMMUL8_CRT_ROWS=8 (the round-6 kernel) and GEMMUL8_CRT_PF=0/1 (read once) are the A/B switches
+static int crt_env(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+static int crt_rows_real() {
+    static const int v = crt_env("GEMMUL8_CRT_ROWS", 4) == 8 ? 8 : 4;
+    return v;
+}
+static bool crt_prefetch(int rows) {
+    static const int v = crt_env("GEMMUL8_CRT_PF", -1);
+    return v < 0 ? rows == 8 : v != 0;
+}
+template <int OT, bool NUMM1, unsigned N, bool KARA, int R>
+static void launch_crt_r(const CrtArgs &a, dim3 grid, hipStream_t st) {
+    grid.x = (unsigned)((a.m + 256 * R - 1) / (256 * R));
+    if (!KARA && OT < 2 && grid.y < a.n && crt_prefetch(R))
+        launch(crt_kernel<OT, NUMM1, N, KARA, R, true>, grid, dim3(256), st, a);
+    else
+        launch(crt_kernel<OT, NUMM1, N, KARA, R>, grid, dim3(256), st, a);
+}
 template <int OT, bool NUMM1, unsigned N, bool KARA>
 static void launch_crt_n(const CrtArgs &a, dim3 grid, hipStream_t st) {
-    constexpr int R = KARA ? OZ2_KARA_ROWS : CRT_ROWS;
-    grid.x = (unsigned)((a.m + 256 * R - 1) / (256 * R));
-    if (!KARA && OT < 2 && grid.y < a.n) launch(crt_kernel<OT, NUMM1, N, KARA, R, true>, grid, dim3(256), st, a);
-    else launch(crt_kernel<OT, NUMM1, N, KARA, R>, grid, dim3(256), st, a);
+    if (!KARA && OT < 2 && crt_rows_real() == 4) launch_crt_r<OT, NUMM1, N, KARA, 4>(a, grid, st);
+    else launch_crt_r<OT, NUMM1, N, KARA, KARA ? OZ2_KARA_ROWS : CRT_ROWS>(a, grid, st);
 }
 
 template <int OT, bool NUMM1, bool KARA = false>

@@ -99,6 +99,9 @@ template <typename R> __device__ __forceinline__ R add_ru(R a, R b);
 template <> __device__ __forceinline__ double add_ru<double>(double a, double b) { return __dadd_ru(a, b); }
 template <> __device__ __forceinline__ float add_ru<float>(float a, float b) { return __fadd_ru(a, b); }
 
+#ifndef OZ2_STATS_XCD
+#define OZ2_STATS_XCD 1  // A/B builds: 0 = strided stats blocks in dispatch order (no XCD renumbering)
+#endif
 // loads in flight per thread in the stats passes (probe builds vary them: tools/probes/stats_probe.hip, in git
 // history at ae0caaa)
 #ifndef OZ2_STRIDED_LOADS
@@ -365,11 +368,19 @@ __device__ __forceinline__ void stats_strided_body(const R *__restrict__ X, size
         if (lane == 0 && v2 < nvec) sft_out[v2] = (int16_t)(-compute_sft(mx, nrm, log2M));
     }
 }
+// Blocks of fewer than 16 rows share the 128-byte lines of a strided sweep (16 f64 rows) with their neighbours: the
+// blocks the dispatcher deals round-robin over the 8 XCDs are renumbered so that neighbours run on one XCD and its L2
+// serves the line once (xcd_local_block: the GEMM's bijective XCD remap, over the first `nb` blocks)
+__device__ __forceinline__ unsigned xcd_local_block(unsigned bid, unsigned nb) {
+    const unsigned xcd = bid & 7, q8 = nb >> 3, r8 = nb & 7;
+    return (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+}
 template <typename R, bool CPLX, int VT, bool ACCU, int ROWS, bool NT>
 __global__ __launch_bounds__(256) void stats_strided_kernel(const R *__restrict__ X, size_t ld, size_t len, size_t nvec,
                                                            float log2M, int16_t *__restrict__ sft_out) {
     __shared__ StridedShared<R, VT, ROWS> sh;
-    stats_strided_body<R, CPLX, VT, ACCU, ROWS, NT>(X, ld, len, nvec, log2M, sft_out, blockIdx.x, sh);
+    const unsigned bx = ROWS < 16 && OZ2_STATS_XCD ? xcd_local_block(blockIdx.x, gridDim.x) : blockIdx.x;
+    stats_strided_body<R, CPLX, VT, ACCU, ROWS, NT>(X, ld, len, nvec, log2M, sft_out, bx, sh);
 }
 
 // Both operands' fast-mode shifts in one launch (small problems, one stream; real f64, A rows strided,
@@ -384,7 +395,9 @@ __global__ __launch_bounds__(256) void stats_pair_kernel(const double *__restric
     __shared__ double grp[2][32];
     __shared__ double gmax[2][8];
     if (blockIdx.x < ga) {
-        stats_strided_body<double, false, 128, false, ROWS, NT>(A, lda, len, m, log2M, sftA, blockIdx.x, sh);
+        // (the A blocks come first, so their block id modulo 8 is their XCD)
+        const unsigned bx = ROWS < 16 && OZ2_STATS_XCD ? xcd_local_block(blockIdx.x, ga) : blockIdx.x;
+        stats_strided_body<double, false, 128, false, ROWS, NT>(A, lda, len, m, log2M, sftA, bx, sh);
     } else {
         const int half = threadIdx.x >> 7;
         const size_t v = 2 * (size_t)(blockIdx.x - ga) + half;

@@ -12,7 +12,7 @@ import time
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-sys.path.insert(0, os.path.join(ROOT, "mixed-gemmul8_amd"))
+sys.path.insert(0, os.environ.get("SMALL_PKG") or os.path.join(ROOT, "mixed-gemmul8_amd"))
 import gemmul8 as G  # noqa: E402
 
 
