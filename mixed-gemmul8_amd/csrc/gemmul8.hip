@@ -285,12 +285,19 @@ static void phase_bound(const Call &c, const Views &v, size_t c0 = 0, size_t c1 
     // per-tile exponents in slice plane 1, unused until the final encode (GEMMUL8_ONE_READ_MAGNITUDES=0: the
     // reference's two reads, for A/B runs)
     const size_t s1A = v.L.S >= 2 ? L.planeA : 0, s1B = v.L.S >= 2 ? L.planeB : 0;
-    if (sft0_ready || !one_read_magnitudes() ||
+    // one stream (small problems): both operands' magnitudes in two launches, the bound maxima zeroed by the second
+    const bool pair = !c.lane && !sft0_ready && one_read_magnitudes() &&
+                      split_magnitudes_pair(c.A, c.m, c.B, c.n, c.k, v.sft0, v.sft0 + L.m_pad, v.A8, v.B8, L,
+                                            v.A8 + L.planeA, s1A, v.B8 + L.planeB, s1B, v.bound, L.m_pad + L.n_pad,
+                                            c.st);
+    if (pair) {
+    } else if (sft0_ready || !one_read_magnitudes() ||
         !split_magnitudes(c.A, true, c.m, c.k, v.sft0, v.A8, L, v.A8 + L.planeA, s1A, c.st)) {
         if (!sft0_ready) split_stats(c.A, c.k, c.m, c.VT, true, 0.f, v.sft0, c.st);
         split_encode(c.A, true, c.m, c.k, v.sft0, v.A8, L.planeA, L, 1, MP, c.st);
     }
-    if (sft0_ready || !one_read_magnitudes() ||
+    if (pair) {
+    } else if (sft0_ready || !one_read_magnitudes() ||
         !split_magnitudes(c.B, false, c.n, c.k, v.sft0 + L.m_pad, v.B8, L, v.B8 + L.planeB, s1B, c.stB)) {
         if (!sft0_ready) split_stats(c.B, c.k, c.n, c.VT, true, 0.f, v.sft0 + L.m_pad, c.stB);
         // big-matrix B magnitudes carry the reference's tail defect; classic / Karatsuba do not
@@ -299,7 +306,7 @@ static void phase_bound(const Call &c, const Views &v, size_t c0 = 0, size_t c1 
                      c.cplx && c.ctype == GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE && c.B.contig);
     }
     join(c);
-    zero_i32(v.bound, L.m_pad + L.n_pad, c.st);
+    if (!pair) zero_i32(v.bound, L.m_pad + L.n_pad, c.st);
     if (c1 > c.n) c1 = c.n;
     if (c0 == 0 && c1 == c.n) {
         gemm_i8(v.A8, v.B8, L, 1, Epi::BOUND, nullptr, v.bound, v.bound + L.m_pad, MP, c.st);
@@ -345,8 +352,13 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
     if (!c.lane) {
         // one stream (small problems): both operands' shifts, then both operands' slices, one launch each
         // where the operand forms allow it
-        if (!shifts_ready && !(c.fast && split_stats_pair(c.A, c.m, c.B, c.n, c.k, c.VT, oz2_log2M_fast[c.N - 2],
-                                                          v.sftA, v.sftB, c.st))) {
+        if (shifts_ready) {
+        } else if (!c.fast && !c.cplx) {
+            const size_t bm = v.L.bm_pad;
+            split_finalize_accurate_pair(v.sft0, v.bound, c.m, v.sft0 + bm, v.bound + bm, c.n,
+                                         oz2_log2M_accu[c.N - 2], v.sftA, v.sftB, c.st);
+        } else if (!(c.fast && split_stats_pair(c.A, c.m, c.B, c.n, c.k, c.VT, oz2_log2M_fast[c.N - 2], v.sftA,
+                                                v.sftB, c.st))) {
             operand_shifts(c, v, true, c.st);
             operand_shifts(c, v, false, c.st);
         }

@@ -92,6 +92,17 @@ bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, si
                       float log2M, int16_t *sftA, int16_t *sftB, hipStream_t st);
 // mode 0 slices of both operands (one element type) in a single launch (false: not applicable,
 // nothing launched)
+// accurate mode, one stream, real operands of one element type: sft0 and the magnitude planes of both operands in
+// two launches (tile pass; fix-up with the vector exponents found in-block), zeroing the bound maxima
+// [0, nbound) on the way; false (nothing launched) where the forms or the scratch do not allow it
+bool split_magnitudes_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
+                           int16_t *sft0A, int16_t *sft0B, int8_t *outA, int8_t *outB, const Layout &L,
+                           void *scratchA, size_t bytesA, void *scratchB, size_t bytesB, int32_t *bound,
+                           size_t nbound, hipStream_t st);
+// both operands' accurate-mode shifts in one launch
+void split_finalize_accurate_pair(const int16_t *sft0A, const int32_t *boundA, size_t m, const int16_t *sft0B,
+                                  const int32_t *boundB, size_t n, float log2M, int16_t *outA, int16_t *outB,
+                                  hipStream_t st);
 bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
                        const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
                        const ModParams &MP, hipStream_t st);

@@ -820,13 +820,13 @@ template <typename R> __device__ __forceinline__ int mag_byte(R y) {
 }
 
 template <typename R, bool CONTIG, bool NTL>
-__global__ __launch_bounds__(256) void mag_tile_kernel(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
-                                                        int8_t *__restrict__ out, size_t ksteps,
-                                                        int2 *__restrict__ tinfo, size_t tstride, int flags) {
-    __shared__ EncTile<R, false> tile;
+__device__ __forceinline__ void mag_tile_body(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                              int8_t *__restrict__ out, size_t ksteps, int2 *__restrict__ tinfo,
+                                              size_t tstride, int flags, unsigned bx, unsigned by,
+                                              EncTile<R, false> &tile) {
     const bool kfirst = CONTIG && (flags & ENC_KFIRST);
-    const size_t kt = kfirst ? blockIdx.x : blockIdx.y;
-    const size_t v0 = (size_t)(kfirst ? blockIdx.y : blockIdx.x) * 64, e0 = kt * 64;
+    const size_t kt = kfirst ? bx : by;
+    const size_t v0 = (size_t)(kfirst ? by : bx) * 64, e0 = kt * 64;
     const int tid = threadIdx.x;
     constexpr int NL = 16;  // 64 x 64 / 256
     const bool interior = v0 + 64 <= nvec && e0 + 64 <= len;
@@ -885,6 +885,13 @@ __global__ __launch_bounds__(256) void mag_tile_kernel(const R *__restrict__ X, 
         tinfo[kt * tstride + v] = make_int2(et, em);
     }
 }
+template <typename R, bool CONTIG, bool NTL>
+__global__ __launch_bounds__(256) void mag_tile_kernel(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                                        int8_t *__restrict__ out, size_t ksteps,
+                                                        int2 *__restrict__ tinfo, size_t tstride, int flags) {
+    __shared__ EncTile<R, false> tile;
+    mag_tile_body<R, CONTIG, NTL>(X, ld, nvec, len, out, ksteps, tinfo, tstride, flags, blockIdx.x, blockIdx.y, tile);
+}
 
 // the vector exponent e_v = max over its tiles of e_t (= ilogb of the vector amax) and sft0 = sft0_of(amax):
 // 64 vectors x 4 tile slices per block
@@ -922,16 +929,32 @@ __global__ __launch_bounds__(256) void mag_vexp_kernel(size_t nvec, size_t ktile
 // bytes of all FIX_T tiles are loaded before any is rewritten (one wave-tile alone left too few bytes in flight:
 // 3.7-3.9 TB/s, profiles/r05/cfg4_single_stream/)
 constexpr int FIX_T = 4;
-template <typename R, bool CONTIG>
-__global__ __launch_bounds__(256) void mag_fixup_kernel(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
-                                                         int8_t *__restrict__ out, size_t ksteps, size_t ktiles,
-                                                         const int2 *__restrict__ tinfo, size_t tstride,
-                                                         const int *__restrict__ vexp) {
+// VEXP: the block finds its vectors' e_v itself (the 8 threads of a vector over every 8th tile, an LDS max;
+// blocks of k-tile group 0 store sft0) instead of reading mag_vexp_kernel's: the small-problem pair launch
+template <typename R, bool CONTIG, bool VEXP = false>
+__device__ __forceinline__ void mag_fixup_body(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                               int8_t *__restrict__ out, size_t ksteps, size_t ktiles,
+                                               const int2 *__restrict__ tinfo, size_t tstride,
+                                               const int *__restrict__ vexp, int16_t *__restrict__ sft0_out,
+                                               unsigned bx, unsigned by, int (*part)[32]) {
     const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-    const size_t v = (size_t)blockIdx.x * 32 + r;
-    const size_t t0 = ((size_t)blockIdx.y * 4 + (threadIdx.x >> 6)) * FIX_T;
+    const size_t v = (size_t)bx * 32 + r;
+    const size_t t0 = ((size_t)by * 4 + (threadIdx.x >> 6)) * FIX_T;
+    int ev;
+    if constexpr (VEXP) {
+        const int q = (threadIdx.x >> 6) * 2 + h;
+        int e = INT_MIN;
+        if (v < nvec)
+            for (size_t t = q; t < ktiles; t += 8) e = max(e, tinfo[t * tstride + v].x);
+        part[q][r] = e;
+        __syncthreads();
+        ev = part[0][r];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) ev = max(ev, part[i][r]);
+        if (by == 0 && threadIdx.x < 32 && v < nvec) sft0_out[v] = sft0_of_exp<R>(ev);
+    }
     if (v >= nvec || t0 >= ktiles) return;  // padding vectors: pass 1 wrote their zeros
-    const int ev = vexp[v];
+    if constexpr (!VEXP) ev = vexp[v];
     uint4 *p0[FIX_T], *p1[FIX_T];
     uint4 b0[FIX_T], b1[FIX_T];
     int2 ti[FIX_T];
@@ -986,6 +1009,55 @@ __global__ __launch_bounds__(256) void mag_fixup_kernel(const R *__restrict__ X,
         }
     }
 }
+template <typename R, bool CONTIG>
+__global__ __launch_bounds__(256) void mag_fixup_kernel(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
+                                                         int8_t *__restrict__ out, size_t ksteps, size_t ktiles,
+                                                         const int2 *__restrict__ tinfo, size_t tstride,
+                                                         const int *__restrict__ vexp) {
+    mag_fixup_body<R, CONTIG>(X, ld, nvec, len, out, ksteps, ktiles, tinfo, tstride, vexp, nullptr, blockIdx.x,
+                              blockIdx.y, nullptr);
+}
+
+// Accurate mode, small problems (one stream): both operands' magnitude passes in two launches instead of six,
+// and both finalizations in one instead of two.  MagOperand: one operand's pass-1 / fix-up geometry.
+struct MagOperand {
+    const void *X;
+    size_t ld, nvec, len, tstride, ktiles;
+    int8_t *out;
+    int2 *tinfo;
+    int16_t *sft0;
+    int flags;
+    unsigned g1x, g1y, g3x, g3y;
+};
+template <typename R, bool CA, bool CB>
+__global__ __launch_bounds__(256) void mag_tile_pair_kernel(MagOperand a, MagOperand b, size_t ksteps) {
+    __shared__ EncTile<R, false> tile;
+    const unsigned na = a.g1x * a.g1y;
+    if (blockIdx.x < na)
+        mag_tile_body<R, CA, false>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.out, ksteps, a.tinfo,
+                                    a.tstride, a.flags, blockIdx.x % a.g1x, blockIdx.x / a.g1x, tile);
+    else {
+        const unsigned t = blockIdx.x - na;
+        mag_tile_body<R, CB, false>(static_cast<const R *>(b.X), b.ld, b.nvec, b.len, b.out, ksteps, b.tinfo,
+                                    b.tstride, b.flags, t % b.g1x, t / b.g1x, tile);
+    }
+}
+// (zeroes the bound maxima too: the bound product that follows accumulates into them with atomicMax)
+template <typename R, bool CA, bool CB>
+__global__ __launch_bounds__(256) void mag_fixup_pair_kernel(MagOperand a, MagOperand b, size_t ksteps,
+                                                              int32_t *__restrict__ bound, size_t nbound) {
+    __shared__ int part[8][32];
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < nbound; i += (size_t)gridDim.x * 256) bound[i] = 0;
+    const unsigned na = a.g3x * a.g3y;
+    if (blockIdx.x < na)
+        mag_fixup_body<R, CA, true>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.out, ksteps, a.ktiles,
+                                    a.tinfo, a.tstride, nullptr, a.sft0, blockIdx.x % a.g3x, blockIdx.x / a.g3x, part);
+    else {
+        const unsigned t = blockIdx.x - na;
+        mag_fixup_body<R, CB, true>(static_cast<const R *>(b.X), b.ld, b.nvec, b.len, b.out, ksteps, b.ktiles,
+                                    b.tinfo, b.tstride, nullptr, b.sft0, t % b.g3x, t / b.g3x, part);
+    }
+}
 
 // Both operands' slices in one launch (small problems, one stream): blocks [0, gx*gy of A) encode A,
 // the rest B.  Saves a launch boundary and lets A's and B's tiles share the chip.
@@ -1023,6 +1095,20 @@ __global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, c
     const int amax = cplx_rows ? max(bound[v], bound[v + nvec]) : bound[v];
     const int s = sft0_stored(sft0[v]) + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
     sft_out[v] = (int16_t)(-s);
+}
+
+// both operands: vectors [0, nA) of A (sft0A, boundA), then [0, nB) of B
+__global__ void finalize_accurate_pair_kernel(const int16_t *__restrict__ sft0A, const int32_t *__restrict__ boundA,
+                                              size_t nA, const int16_t *__restrict__ sft0B,
+                                              const int32_t *__restrict__ boundB, size_t nB, float log2M,
+                                              int16_t *__restrict__ outA, int16_t *__restrict__ outB) {
+    size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool isA = v < nA;
+    if (!isA) v -= nA;
+    if (!isA && v >= nB) return;
+    const int amax = (isA ? boundA : boundB)[v];
+    const int s = sft0_stored((isA ? sft0A : sft0B)[v]) + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
+    (isA ? outA : outB)[v] = (int16_t)(-s);
 }
 
 // zeroes the accurate-mode bound maxima before the bound product (a kernel rather than
@@ -1170,6 +1256,59 @@ bool split_magnitudes(const OperandDesc &d, bool is_A, size_t nvec, size_t len, 
     else { if (d.contig) OZ2_MG(float, true); else OZ2_MG(float, false); }
 #undef OZ2_MG
     return true;
+}
+
+bool split_magnitudes_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
+                           int16_t *sft0A, int16_t *sft0B, int8_t *outA, int8_t *outB, const Layout &L,
+                           void *scratchA, size_t bytesA, void *scratchB, size_t bytesB, int32_t *bound,
+                           size_t nbound, hipStream_t st) {
+    if (dA.cplx || dB.cplx || dA.dbl != dB.dbl || L.kblk == 0 || m == 0 || n == 0) return false;
+    const size_t ktiles = L.kblk / 64;
+    auto operand = [&](const OperandDesc &d, size_t nvec, size_t vpad_rows, int16_t *sft0, int8_t *out,
+                       void *scratch, size_t bytes, MagOperand &o) {
+        const size_t vpad = round_up(vpad_rows, 64);
+        if (bytes < ktiles * vpad * sizeof(int2) || (d.contig && vpad / 64 > 65536)) return false;
+        o.X = d.ptr;
+        o.ld = d.ld;
+        o.nvec = nvec;
+        o.len = len;
+        o.tstride = vpad;
+        o.ktiles = ktiles;
+        o.out = out;
+        o.tinfo = static_cast<int2 *>(scratch);
+        o.sft0 = sft0;
+        o.flags = d.contig ? ENC_KFIRST : 0;
+        o.g1x = d.contig ? (unsigned)ktiles : (unsigned)(vpad / 64);
+        o.g1y = d.contig ? (unsigned)(vpad / 64) : (unsigned)ktiles;
+        o.g3x = (unsigned)((nvec + 31) / 32);
+        o.g3y = (unsigned)((ktiles + 4 * FIX_T - 1) / (4 * FIX_T));
+        return true;
+    };
+    MagOperand a{}, b{};
+    if (!operand(dA, m, L.m_pad, sft0A, outA, scratchA, bytesA, a) ||
+        !operand(dB, n, L.n_pad, sft0B, outB, scratchB, bytesB, b))
+        return false;
+    const size_t g1 = (size_t)a.g1x * a.g1y + (size_t)b.g1x * b.g1y, g3 = (size_t)a.g3x * a.g3y + (size_t)b.g3x * b.g3y;
+    if (g1 > 0x7fffffff || g3 > 0x7fffffff) return false;
+#define OZ2_MP(R, CA, CB) do { \
+        launch(mag_tile_pair_kernel<R, CA, CB>, dim3((unsigned)g1), dim3(256), st, a, b, L.ksteps); \
+        launch(mag_fixup_pair_kernel<R, CA, CB>, dim3((unsigned)g3), dim3(256), st, a, b, L.ksteps, bound, nbound); \
+    } while (0)
+#define OZ2_MPR(R) do { if (dA.contig) { if (dB.contig) OZ2_MP(R, true, true); else OZ2_MP(R, true, false); } \
+                        else { if (dB.contig) OZ2_MP(R, false, true); else OZ2_MP(R, false, false); } } while (0)
+    if (dA.dbl) OZ2_MPR(double);
+    else OZ2_MPR(float);
+#undef OZ2_MPR
+#undef OZ2_MP
+    return true;
+}
+
+void split_finalize_accurate_pair(const int16_t *sft0A, const int32_t *boundA, size_t m, const int16_t *sft0B,
+                                  const int32_t *boundB, size_t n, float log2M, int16_t *outA, int16_t *outB,
+                                  hipStream_t st) {
+    if (m + n == 0) return;
+    launch(finalize_accurate_pair_kernel, dim3((unsigned)((m + n + 255) / 256)), dim3(256), st, sft0A, boundA, m,
+           sft0B, boundB, n, log2M, outA, outB);
 }
 
 bool split_stats_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
