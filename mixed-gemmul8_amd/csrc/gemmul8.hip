@@ -350,8 +350,16 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
                         bool shifts_ready = false) {
     if (!c.fast && !bound_ready && !shifts_ready) phase_bound(c, v);
     if (!c.lane) {
-        // one stream (small problems): both operands' shifts, then both operands' slices, one launch each
-        // where the operand forms allow it
+        // one stream (small problems): fast mode, k <= 2048: shifts and slices in one launch; otherwise both
+        // operands' shifts, then both operands' slices, one launch each where the operand forms allow it
+        if (c.fast && !shifts_ready && j1 > j0) {
+            const Layout &L = v.L;
+            ModParams SP = sub_mod_params(c.N, j0, j1);
+            SP.zero_queue = queue_of(v, j0);
+            if (split_fused_pair(c.A, c.m, c.B, c.n, c.k, c.VT, oz2_log2M_fast[c.N - 2], v.sftA, v.sftB,
+                                 v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB, L, SP, c.st))
+                return;
+        }
         if (shifts_ready) {
         } else if (!c.fast && !c.cplx) {
             const size_t bm = v.L.bm_pad;

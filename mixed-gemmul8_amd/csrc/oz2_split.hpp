@@ -103,6 +103,12 @@ bool split_magnitudes_pair(const OperandDesc &dA, size_t m, const OperandDesc &d
 void split_finalize_accurate_pair(const int16_t *sft0A, const int32_t *boundA, size_t m, const int16_t *sft0B,
                                   const int32_t *boundB, size_t n, float log2M, int16_t *outA, int16_t *outB,
                                   hipStream_t st);
+// fast mode, one stream, real f64, VT = 128, k <= 2048: both operands' shifts and slices of the moduli in MP in one
+// launch reading each operand once (split_fused_kernel); false (nothing launched) where it does not apply
+// (GEMMUL8_FUSED_SPLIT=0: never)
+bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
+                      float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
+                      const ModParams &MP, hipStream_t st);
 bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
                        const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
                        const ModParams &MP, hipStream_t st);

@@ -1087,6 +1087,123 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_pair_kernel(EncOperan
     }
 }
 
+// ------------------------------------------------------------------
+// Fast mode, small k, one stream: shifts and slices of both operands in ONE launch that reads each operand once.
+// A block holds FZ_V = 4 (GEMMUL8_FUSED_V=8: 8) whole vectors (k <= KMAX elements each, f64) in LDS: it loads them (coalesced along
+// whichever index is contiguous), sums them in the reference's order -- wave w takes vector w, lane l the
+// reference's virtual threads l and l + 64 of VT = 128 (their round-up chains in element order), then the
+// tail of stats_strided_body -- and encodes its vectors from the same LDS copy (encode_vec16, MODE 0).  Same
+// shifts and bytes as split_stats_pair + split_encode_pair (tests/test_gpu_parity.py), one launch and one
+// operand read instead of two each.  Blocks [0, na) take A's vectors, the rest B's.
+// ------------------------------------------------------------------
+struct FusedOperand {
+    const double *X;
+    size_t ld, nvec, vpad, plane, vmax;
+    int16_t *sft;
+    int8_t *out;
+};
+template <int KMAX, int FZ_V, bool CONTIG>
+__device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, size_t len, size_t ksteps, size_t kblk,
+                                           float log2M, const ModParams &MP, const ModGroups &G, unsigned bx,
+                                           double (&panel)[FZ_V][KMAX + 2], int (&shl)[FZ_V]) {
+    constexpr int FZ_NT = 64 * FZ_V;  // one wave per vector
+    static_assert(KMAX % 128 == 0 && KMAX % FZ_NT == 0, "whole chains and load rounds");
+    const int tid = threadIdx.x;
+    const size_t v0 = (size_t)bx * FZ_V;
+    // stage the vectors: zeros past len and past nvec
+    if (CONTIG) {
+        // vector j's elements e = tid + FZ_NT i: each wave load is 512 contiguous bytes
+        constexpr int PER = KMAX / FZ_NT;
+#pragma unroll
+        for (int j = 0; j < FZ_V; ++j) {
+            double x[PER > 0 ? PER : 1];
+            const size_t v = v0 + j;
+#pragma unroll
+            for (int i = 0; i < PER; ++i) {
+                const size_t e = tid + (size_t)FZ_NT * i;
+                x[i] = v < o.nvec && e < len ? o.X[v * o.ld + e] : 0.0;
+            }
+#pragma unroll
+            for (int i = 0; i < PER; ++i) panel[j][tid + FZ_NT * i] = x[i];
+        }
+    } else {
+        // row r = tid mod FZ_V of column e = tid / FZ_V + 64 i: 8 FZ_V contiguous bytes per column
+        constexpr int PER = KMAX / (FZ_NT / FZ_V);
+        const int r = tid & (FZ_V - 1), c = tid / FZ_V;
+        const size_t v = v0 + r;
+        double x[PER];
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const size_t e = c + (size_t)(FZ_NT / FZ_V) * i;
+            x[i] = v < o.nvec && e < len ? o.X[e * o.ld + v] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < PER; ++i) panel[r][c + (FZ_NT / FZ_V) * i] = x[i];
+    }
+    __syncthreads();
+    {
+        // wave w: vector v0 + w; lane l: the chains of virtual threads l and l + 64 (elements vt + 128 i, in order)
+        const int w = tid >> 6, lane = tid & 63;
+        double a0 = 0, a1 = 0, amax = 0;
+        for (int i = 0; i < KMAX / 128; ++i) {
+            const double x0 = fabs(panel[w][lane + 128 * i]), x1 = fabs(panel[w][lane + 64 + 128 * i]);
+            amax = fmax(amax, fmax(x0, x1));
+            a0 = sq_add_ru<double>(x0, a0);
+            a1 = sq_add_ru<double>(x1, a1);
+        }
+        const double mx = wave_max<double>(amax);
+        const double s0 = ref_wave_sum<double>(a0), s1 = ref_wave_sum<double>(a1);
+        const double g00 = __shfl(s0, 1), g01 = __shfl(s0, 33), g10 = __shfl(s1, 1), g11 = __shfl(s1, 33);
+        double gv = lane == 32 ? g00 : lane == 33 ? g01 : lane == 34 ? g10 : lane == 35 ? g11 : 0.0;
+        gv = ref_wave_sum<double>(gv);
+        const double nrm = __shfl(gv, 32);
+        const size_t v = v0 + w;
+        if (lane == 0) {
+            int sh = 0;
+            if (v < o.nvec) {
+                const int16_t st = (int16_t)(-compute_sft(mx, nrm, log2M));
+                o.sft[v] = st;
+                sh = -(int)st;
+            }
+            shl[w] = sh;
+        }
+    }
+    __syncthreads();
+    // encode: thread (vector tid mod FZ_V, 16-element chunk tid / FZ_V): FZ_V x 16 contiguous panel bytes
+    const int r = tid & (FZ_V - 1), c = tid / FZ_V;
+    const size_t v = v0 + r;
+    const int sh = shl[r];
+    for (size_t kk = 16 * (size_t)c; kk < kblk; kk += 16 * (FZ_NT / FZ_V)) {
+        double yr[16], yi[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            yr[q] = trunc(scalbn(panel[r][kk + q], sh));
+            yi[q] = 0;
+        }
+        if (is_a) encode_vec16<double, false, true, 0>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
+        else encode_vec16<double, false, false, 0>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
+    }
+}
+template <int KMAX, int FZ_V, bool CA, bool CB>
+__global__ __launch_bounds__(64 * FZ_V) void split_fused_kernel(FusedOperand a, FusedOperand b, size_t len,
+                                                                size_t ksteps, size_t kblk, float log2M, ModParams MP,
+                                                                ModGroups G) {
+    __shared__ double panel[FZ_V][KMAX + 2];
+    __shared__ int shl[FZ_V];
+    if (MP.zero_queue && blockIdx.x == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
+    const unsigned na = (unsigned)(a.vpad / FZ_V), nb = (unsigned)(b.vpad / FZ_V);
+    // (na and nb are multiples of 8 (vpad of 64): a strided operand's neighbouring blocks, which share 128-byte lines, are
+    // renumbered onto one XCD)
+    if (blockIdx.x < na) {
+        const unsigned bx = CA ? blockIdx.x : xcd_local_block(blockIdx.x, na);
+        fused_body<KMAX, FZ_V, CA>(a, true, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+    } else {
+        const unsigned t = blockIdx.x - na;
+        const unsigned bx = CB ? t : xcd_local_block(t, nb);
+        fused_body<KMAX, FZ_V, CB>(b, false, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+    }
+}
+
 // accurate mode: sft = sft0 + floor_rd(-0.51*log2(amax) + log2M)  (int8tc::compute_sft, scaling.hpp:1504-1506)
 __global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, const int32_t *__restrict__ bound,
                                              size_t nvec, float log2M, int16_t *__restrict__ sft_out, int cplx_rows) {
@@ -1300,6 +1417,56 @@ bool split_magnitudes_pair(const OperandDesc &dA, size_t m, const OperandDesc &d
     else OZ2_MPR(float);
 #undef OZ2_MPR
 #undef OZ2_MP
+    return true;
+}
+
+static int fused_split_mode() {  // GEMMUL8_FUSED_SPLIT=0: the two-launch split (A/B runs)
+    static const int v = [] {
+        const char *e = getenv("GEMMUL8_FUSED_SPLIT");
+        return e ? atoi(e) : 1;
+    }();
+    return v;
+}
+bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
+                      float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
+                      const ModParams &MP, hipStream_t st) {
+    if (!fused_split_mode() || dA.cplx || dB.cplx || !dA.dbl || !dB.dbl || VT != 128 || L.kara || L.kblk == 0 ||
+        L.kblk > 2048 || m == 0 || n == 0)
+        return false;
+    FusedOperand a{}, b{};
+    a.X = static_cast<const double *>(dA.ptr);
+    a.ld = dA.ld;
+    a.nvec = m;
+    a.vpad = round_up(L.m_pad, 64);
+    a.plane = L.planeA;
+    a.vmax = L.m_pad;
+    a.sft = sftA;
+    a.out = outA;
+    b.X = static_cast<const double *>(dB.ptr);
+    b.ld = dB.ld;
+    b.nvec = n;
+    b.vpad = round_up(L.n_pad, 64);
+    b.plane = L.planeB;
+    b.vmax = L.n_pad;
+    b.sft = sftB;
+    b.out = outB;
+    // vectors per block: GEMMUL8_FUSED_V = 4 / 8 (read once), by default 4
+    static const int fv = [] {
+        const char *e = getenv("GEMMUL8_FUSED_V");
+        return e && atoi(e) == 8 ? 8 : 4;
+    }();
+    const size_t blocks = (a.vpad + b.vpad) / fv;
+    if (blocks > 0x7fffffff) return false;
+    const ModGroups G = make_groups(MP, L.N);
+    const dim3 grid((unsigned)blocks), block(64 * fv);
+#define OZ2_FZ(K, V) do { if (dA.contig) { if (dB.contig) launch(split_fused_kernel<K, V, true, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
+                                            else launch(split_fused_kernel<K, V, true, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } \
+                          else { if (dB.contig) launch(split_fused_kernel<K, V, false, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
+                                 else launch(split_fused_kernel<K, V, false, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } } while (0)
+    if (L.kblk <= 1024) { if (fv == 8) OZ2_FZ(1024, 8); else OZ2_FZ(1024, 4); }
+    else if (L.kblk <= 1536) { if (fv == 8) OZ2_FZ(1536, 8); else OZ2_FZ(1536, 4); }
+    else { if (fv == 8) OZ2_FZ(2048, 8); else OZ2_FZ(2048, 4); }
+#undef OZ2_FZ
     return true;
 }
 

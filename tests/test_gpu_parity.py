@@ -433,6 +433,40 @@ def test_k_chunks_forced(fast):
     assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
 
 
+@pytest.mark.parametrize("m,n,k,opA,opB", [(70, 90, 1100, 0, 0), (33, 130, 1536, 1, 1), (129, 40, 2048, 0, 1),
+                                           (300, 7, 1500, 1, 0), (5, 64, 1024, 0, 0)])
+def test_fused_split_long_k(m, n, k, opA, opB):
+    """fast mode, one stream, k in (1024, 2048] and at 1024: the one-launch split (split_fused_kernel, 1536- and
+    2048-element panels) for every operand form (strided / contiguous vectors): shifts, slices, residues and C
+    against the oracle, with an all-zero row of op(A) and column of op(B) among the vectors"""
+    rng = np.random.default_rng(m + n + k + opA + opB)
+    A = randmat_np(rng, k, m) if opA else randmat_np(rng, m, k)
+    B = randmat_np(rng, n, k) if opB else randmat_np(rng, k, n)
+    if m > 3 and n > 3:
+        (A[:, 1] if opA else A[1, :])[:] = 0.0
+        (B[2, :] if opB else B[:, 2])[:] = 0.0
+    check_full(A, B, 14, opA=opA, opB=opB)
+
+
+@pytest.mark.parametrize("env", [{"GEMMUL8_FUSED_V": "8"}, {"GEMMUL8_FUSED_SPLIT": "0"}])
+def test_fused_split_variants(env):
+    """the one-launch split with 8 vectors per block and the two-launch split (child processes): the same
+    shifts, slices and C as the oracle at k = 1024, 1536 and 2048"""
+    import subprocess
+    code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
+            "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
+            "rng = np.random.default_rng(9)\n"
+            "check_full(randmat_np(rng, 70, 1024), randmat_np(rng, 1024, 90), 14)\n"
+            "check_full(randmat_np(rng, 1536, 33), randmat_np(rng, 130, 1536), 14, opA=1, opB=1)\n"
+            "check_full(randmat_np(rng, 129, 2000), randmat_np(rng, 40, 2000), 8, opB=1)\n"
+            "print('OK')")
+    tdir = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(tdir)
+    r = subprocess.run([sys.executable, "-c", code, tdir, root, os.path.join(root, "mixed-gemmul8_amd")],
+                       env=dict(os.environ, **env), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stderr[-3000:]
+
+
 def test_complex_karatsuba_products_forced():
     """GEMMUL8_CPLX_PRODUCTS=karatsuba (child process): complex products as Karatsuba sub-products
     at shapes where the size rule keeps the big matrix; Karatsuba slices, the three residue
