@@ -200,6 +200,25 @@ template <> __device__ __forceinline__ float sq_add_ru<float>(float x, float s) 
     return s;
 }
 
+// Two chains of four round-up steps each (s0 += x[i]^2, s1 += y[i]^2 in order i, rounded upward) under ONE mode
+// switch: the same instructions and roundings as eight sq_add_ru, for a wave that runs the chains alone (the
+// fused split's vectors), where each switch's pipeline drain sat on the critical path.
+__device__ __forceinline__ void sq_add4x2_ru(const double (&x)[4], const double (&y)[4], double &s0, double &s1) {
+    asm("s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 1\n\t"
+        "v_fma_f64 %0, %2, %2, %0\n\t"
+        "v_fma_f64 %1, %6, %6, %1\n\t"
+        "v_fma_f64 %0, %3, %3, %0\n\t"
+        "v_fma_f64 %1, %7, %7, %1\n\t"
+        "v_fma_f64 %0, %4, %4, %0\n\t"
+        "v_fma_f64 %1, %8, %8, %1\n\t"
+        "v_fma_f64 %0, %5, %5, %0\n\t"
+        "v_fma_f64 %1, %9, %9, %1\n\t"
+        "s_nop 0\n\t"
+        "s_setreg_imm32_b32 hwreg(HW_REG_MODE, 2, 2), 0"
+        : "+v"(s0), "+v"(s1)
+        : "v"(x[0]), "v"(x[1]), "v"(x[2]), "v"(x[3]), "v"(y[0]), "v"(y[1]), "v"(y[2]), "v"(y[3]));
+}
+
 // SUM = false: the accurate-mode pass, which needs amax only
 template <typename R, bool CPLX, bool SUM = true>
 __device__ __forceinline__ void accum(R re, R im, R &amax, R &sum) {
@@ -1096,18 +1115,28 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_pair_kernel(EncOperan
 // shifts and bytes as split_stats_pair + split_encode_pair (tests/test_gpu_parity.py), one launch and one
 // operand read instead of two each.  Blocks [0, na) take A's vectors, the rest B's.
 // ------------------------------------------------------------------
+// A/B builds (profiles/r06/fused_split/): OZ2_FZ_PAD=1 pads 16 bytes after every 16 elements of the LDS panel
+// (the encode's chunks 144 bytes apart), OZ2_FZ_XCD_CONTIG=1 renumbers a contiguous operand's blocks onto one
+// XCD as the strided operand's are; both measured slower (1536^3 split 33.5 -> 40.5 us with both)
+#ifndef OZ2_FZ_PAD
+#define OZ2_FZ_PAD 0
+#endif
+#ifndef OZ2_FZ_XCD_CONTIG
+#define OZ2_FZ_XCD_CONTIG 0
+#endif
+__device__ __forceinline__ int fz_idx(int e) { return OZ2_FZ_PAD ? e + 2 * (e >> 4) : e; }
+template <int KMAX> constexpr int FZ_ROW = KMAX + (OZ2_FZ_PAD ? KMAX / 8 : 0) + 2;
 struct FusedOperand {
     const double *X;
     size_t ld, nvec, vpad, plane, vmax;
     int16_t *sft;
     int8_t *out;
 };
-template <int KMAX, int FZ_V, bool CONTIG>
+template <int KMAX, int FZ_V, int FZ_NT, bool CONTIG, bool NTL>
 __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, size_t len, size_t ksteps, size_t kblk,
                                            float log2M, const ModParams &MP, const ModGroups &G, unsigned bx,
-                                           double (&panel)[FZ_V][KMAX + 2], int (&shl)[FZ_V]) {
-    constexpr int FZ_NT = 64 * FZ_V;  // one wave per vector
-    static_assert(KMAX % 128 == 0 && KMAX % FZ_NT == 0, "whole chains and load rounds");
+                                           double (&panel)[FZ_V][FZ_ROW<KMAX>], int (&shl)[FZ_V]) {
+    static_assert(KMAX % 128 == 0 && KMAX % FZ_NT == 0 && FZ_NT >= 64 * FZ_V, "whole chains and load rounds");
     const int tid = threadIdx.x;
     const size_t v0 = (size_t)bx * FZ_V;
     // stage the vectors: zeros past len and past nvec
@@ -1121,10 +1150,12 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
                 const size_t e = tid + (size_t)FZ_NT * i;
-                x[i] = v < o.nvec && e < len ? o.X[v * o.ld + e] : 0.0;
+                double im;
+                x[i] = 0.0;
+                if (v < o.nvec && e < len) load_elem<double, false, NTL>(o.X, v * o.ld + e, x[i], im);
             }
 #pragma unroll
-            for (int i = 0; i < PER; ++i) panel[j][tid + FZ_NT * i] = x[i];
+            for (int i = 0; i < PER; ++i) panel[j][fz_idx(tid + FZ_NT * i)] = x[i];
         }
     } else {
         // row r = tid mod FZ_V of column e = tid / FZ_V + 64 i: 8 FZ_V contiguous bytes per column
@@ -1135,21 +1166,30 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const size_t e = c + (size_t)(FZ_NT / FZ_V) * i;
-            x[i] = v < o.nvec && e < len ? o.X[e * o.ld + v] : 0.0;
+            double im;
+            x[i] = 0.0;
+            if (v < o.nvec && e < len) load_elem<double, false, NTL>(o.X, e * o.ld + v, x[i], im);
         }
 #pragma unroll
-        for (int i = 0; i < PER; ++i) panel[r][c + (FZ_NT / FZ_V) * i] = x[i];
+        for (int i = 0; i < PER; ++i) panel[r][fz_idx(c + (FZ_NT / FZ_V) * i)] = x[i];
     }
     __syncthreads();
     {
-        // wave w: vector v0 + w; lane l: the chains of virtual threads l and l + 64 (elements vt + 128 i, in order)
+        // wave w < FZ_V: vector v0 + w; lane l: the chains of virtual threads l and l + 64 (elements vt + 128 i, in
+        // order)
         const int w = tid >> 6, lane = tid & 63;
+        if (w < FZ_V) {
         double a0 = 0, a1 = 0, amax = 0;
-        for (int i = 0; i < KMAX / 128; ++i) {
-            const double x0 = fabs(panel[w][lane + 128 * i]), x1 = fabs(panel[w][lane + 64 + 128 * i]);
-            amax = fmax(amax, fmax(x0, x1));
-            a0 = sq_add_ru<double>(x0, a0);
-            a1 = sq_add_ru<double>(x1, a1);
+        static_assert(KMAX % 512 == 0, "chains in groups of four");
+        for (int i = 0; i < KMAX / 128; i += 4) {
+            double x0[4], x1[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                x0[u] = fabs(panel[w][fz_idx(lane + 128 * (i + u))]);
+                x1[u] = fabs(panel[w][fz_idx(lane + 64 + 128 * (i + u))]);
+                amax = fmax(amax, fmax(x0[u], x1[u]));
+            }
+            sq_add4x2_ru(x0, x1, a0, a1);
         }
         const double mx = wave_max<double>(amax);
         const double s0 = ref_wave_sum<double>(a0), s1 = ref_wave_sum<double>(a1);
@@ -1167,6 +1207,7 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
             }
             shl[w] = sh;
         }
+        }
     }
     __syncthreads();
     // encode: thread (vector tid mod FZ_V, 16-element chunk tid / FZ_V): FZ_V x 16 contiguous panel bytes
@@ -1177,30 +1218,30 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
         double yr[16], yi[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            yr[q] = trunc(scalbn(panel[r][kk + q], sh));
+            yr[q] = trunc(scalbn(panel[r][fz_idx((int)kk) + q], sh));
             yi[q] = 0;
         }
         if (is_a) encode_vec16<double, false, true, 0>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
         else encode_vec16<double, false, false, 0>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
     }
 }
-template <int KMAX, int FZ_V, bool CA, bool CB>
-__global__ __launch_bounds__(64 * FZ_V) void split_fused_kernel(FusedOperand a, FusedOperand b, size_t len,
-                                                                size_t ksteps, size_t kblk, float log2M, ModParams MP,
-                                                                ModGroups G) {
-    __shared__ double panel[FZ_V][KMAX + 2];
+template <int KMAX, int FZ_V, int FZ_NT, bool CA, bool CB, bool NTL = false>
+__global__ __launch_bounds__(FZ_NT) void split_fused_kernel(FusedOperand a, FusedOperand b, size_t len,
+                                                            size_t ksteps, size_t kblk, float log2M, ModParams MP,
+                                                            ModGroups G) {
+    __shared__ double panel[FZ_V][FZ_ROW<KMAX>];
     __shared__ int shl[FZ_V];
     if (MP.zero_queue && blockIdx.x == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
     const unsigned na = (unsigned)(a.vpad / FZ_V), nb = (unsigned)(b.vpad / FZ_V);
-    // (na and nb are multiples of 8 (vpad of 64): a strided operand's neighbouring blocks, which share 128-byte lines, are
-    // renumbered onto one XCD)
+    // (na and nb are multiples of 8 (vpad of 64): a strided operand's neighbouring blocks, which share its 128-byte
+    // input lines, are renumbered onto one XCD)
     if (blockIdx.x < na) {
-        const unsigned bx = CA ? blockIdx.x : xcd_local_block(blockIdx.x, na);
-        fused_body<KMAX, FZ_V, CA>(a, true, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+        const unsigned bx = CA && !OZ2_FZ_XCD_CONTIG ? blockIdx.x : xcd_local_block(blockIdx.x, na);
+        fused_body<KMAX, FZ_V, FZ_NT, CA, NTL>(a, true, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
     } else {
         const unsigned t = blockIdx.x - na;
-        const unsigned bx = CB ? t : xcd_local_block(t, nb);
-        fused_body<KMAX, FZ_V, CB>(b, false, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+        const unsigned bx = CB && !OZ2_FZ_XCD_CONTIG ? t : xcd_local_block(t, nb);
+        fused_body<KMAX, FZ_V, FZ_NT, CB, NTL>(b, false, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
     }
 }
 
@@ -1459,10 +1500,10 @@ bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, si
     if (blocks > 0x7fffffff) return false;
     const ModGroups G = make_groups(MP, L.N);
     const dim3 grid((unsigned)blocks), block(64 * fv);
-#define OZ2_FZ(K, V) do { if (dA.contig) { if (dB.contig) launch(split_fused_kernel<K, V, true, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
-                                            else launch(split_fused_kernel<K, V, true, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } \
-                          else { if (dB.contig) launch(split_fused_kernel<K, V, false, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
-                                 else launch(split_fused_kernel<K, V, false, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } } while (0)
+#define OZ2_FZ(K, V) do { if (dA.contig) { if (dB.contig) launch(split_fused_kernel<K, V, 64 * V, true, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
+                                            else launch(split_fused_kernel<K, V, 64 * V, true, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } \
+                          else { if (dB.contig) launch(split_fused_kernel<K, V, 64 * V, false, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
+                                 else launch(split_fused_kernel<K, V, 64 * V, false, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } } while (0)
     if (L.kblk <= 1024) { if (fv == 8) OZ2_FZ(1024, 8); else OZ2_FZ(1024, 4); }
     else if (L.kblk <= 1536) { if (fv == 8) OZ2_FZ(1536, 8); else OZ2_FZ(1536, 4); }
     else { if (fv == 8) OZ2_FZ(2048, 8); else OZ2_FZ(2048, 4); }

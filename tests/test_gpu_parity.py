@@ -448,6 +448,28 @@ def test_fused_split_long_k(m, n, k, opA, opB):
     check_full(A, B, 14, opA=opA, opB=opB)
 
 
+@pytest.mark.parametrize("m,n,k,opA,opB", [(64, 4096, 8192, 0, 0), (4100, 48, 8000, 1, 1), (3000, 2000, 4100, 1, 0)])
+def test_large_split_forms(m, n, k, opA, opB):
+    """fast mode at (m + n) k >= 2^25, 2048 < k <= 8192: A op N x B op N through the pair kernels, the other forms
+    with the operands on two streams (per-operand stats pass + encode).  Shifts and every slice against the
+    oracle (the products and the CRT downstream are the ones the other tests check)."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(m + n + k)
+    A = randmat_np(rng, k, m) if opA else randmat_np(rng, m, k)
+    B = randmat_np(rng, n, k) if opB else randmat_np(rng, k, n)
+    N = 14
+    _, wsb, L = run_gpu(A, B, N, True, opA, opB)
+    A8o, B8o, sAo, sBo = O.scaling(np.asfortranarray(A), np.asfortranarray(B), N, True, opA, opB)
+    sA, sB = ws_sft(wsb, L, m, n)
+    assert np.array_equal(sA, sAo) and np.array_equal(sB, sBo)
+    for which, X8o, vpad, nv in (("A", A8o, L["m_pad"], m), ("B", B8o, L["n_pad"], n)):
+        planes = ws_planes(wsb, L, N, which)
+        for j in range(N):
+            exp = np.zeros((vpad, L["k_pad"]), np.int8)
+            exp[:nv, :k] = X8o[j]
+            assert np.array_equal(planes[j], exp), f"{which} slice mismatch modulus {j}"
+
+
 @pytest.mark.parametrize("env", [{"GEMMUL8_FUSED_V": "8"}, {"GEMMUL8_FUSED_SPLIT": "0"}])
 def test_fused_split_variants(env):
     """the one-launch split with 8 vectors per block and the two-launch split (child processes): the same
