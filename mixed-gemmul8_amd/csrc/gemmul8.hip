@@ -360,6 +360,17 @@ static void phase_split(const Call &c, const Views &v, unsigned j0, unsigned j1,
                                  v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB, L, SP, c.st))
                 return;
         }
+        if (!c.fast && !c.cplx && !shifts_ready && j1 > j0) {
+            // accurate mode: the final shifts inside the pair encode
+            const Layout &L = v.L;
+            const size_t bm = L.bm_pad;
+            ModParams SP = sub_mod_params(c.N, j0, j1);
+            SP.zero_queue = queue_of(v, j0);
+            const AccurateShifts accs{v.sft0, v.sft0 + bm, v.bound, v.bound + bm, oz2_log2M_accu[c.N - 2]};
+            if (split_encode_pair(c.A, c.m, c.B, c.n, c.k, v.sftA, v.sftB, v.A8 + j0 * L.planeA, v.B8 + j0 * L.planeB,
+                                  L, SP, c.st, &accs))
+                return;
+        }
         if (shifts_ready) {
         } else if (!c.fast && !c.cplx) {
             const size_t bm = v.L.bm_pad;

@@ -14,7 +14,7 @@
 //                                 default fp64_int8_14 (fast mode)
 //   GEMMUL8_COMPUTE_MODE_SGEMM    S and C GEMM: "sgemm" (forward, default) or "fp32_int8_<N>[_accu]"
 //   GEMMUL8_COMPLEX_TYPE          big_matrix (default) | classic | karatsuba
-//   GEMMUL8_INTERCEPT_THRESHOLD_M / _N / _K   emulate only when m, n, k are all >= (default 1536: the
+//   GEMMUL8_INTERCEPT_THRESHOLD_M / _N / _K   emulate only when m, n, k are all >= (default 1280: the
 //                                 measured square crossover on MI355X, below which rocBLAS DGEMM is as fast
 //                                 or faster -- INTEGRATION.md section 3)
 //   GEMMUL8_INFO=1                one line per call on stderr
@@ -156,7 +156,7 @@ Mode parse_mode(const char *name, const char *prefix, bool default_on) {
 struct Config {
     Mode d, s;
     int ctype = GEMMUL8_COMPLEX_BIG_MATRIX_ENCODE;
-    static constexpr long DEFAULT_THRESHOLD = 1536;
+    static constexpr long DEFAULT_THRESHOLD = 1280;
     long tm = DEFAULT_THRESHOLD, tn = DEFAULT_THRESHOLD, tk = DEFAULT_THRESHOLD;
     bool info = false;
     Config() {

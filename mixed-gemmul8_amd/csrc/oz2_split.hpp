@@ -109,9 +109,16 @@ void split_finalize_accurate_pair(const int16_t *sft0A, const int32_t *boundA, s
 bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
                       float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
                       const ModParams &MP, hipStream_t st);
+// accurate mode (real operands): the encode computes the final shifts itself from sft0 and the bound maxima and
+// stores them to sftA / sftB (finalize_accurate_sft_kernel's arithmetic, one launch fewer)
+struct AccurateShifts {
+    const int16_t *sft0A, *sft0B;
+    const int32_t *boundA, *boundB;
+    float log2M;
+};
 bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
                        const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
-                       const ModParams &MP, hipStream_t st);
+                       const ModParams &MP, hipStream_t st, const AccurateShifts *accs = nullptr);
 // cplx_rows: complex A bound of row v = max(bound[v], bound[v + nvec]) (scaling.hpp:2561-2588)
 void split_finalize_accurate(const int16_t *sft0, const int32_t *bound, size_t nvec, float log2M, int16_t *out,
                              hipStream_t st, bool cplx_rows = false);

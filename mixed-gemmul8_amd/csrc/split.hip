@@ -713,11 +713,24 @@ __device__ __forceinline__ void encode_vec16(const R (&yr)[16], const R (&yi)[16
 
 template <typename R, bool CPLX> using EncTile = R[CPLX ? 32 : 64][64 + 1][CPLX ? 2 : 1];
 
-template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE, bool NTL = false>
+// Accurate mode, real operands, one stream: the final shifts computed by the encode itself from sft0 and the bound
+// maxima (finalize_accurate_sft_kernel's arithmetic), stored by the blocks of the first k-tile
+struct AccShift {
+    const int16_t *sft0;
+    const int32_t *bound;
+    int16_t *out;
+    float log2M;
+};
+__device__ __forceinline__ int16_t accurate_sft(int16_t sft0, int32_t amax, float log2M) {
+    const int s = sft0_stored(sft0) + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
+    return (int16_t)(-s);
+}
+template <typename R, bool CPLX, bool CONTIG, bool IS_A, int MODE, bool NTL = false, bool ACC = false>
 __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, size_t nvec, size_t len,
                                             const int16_t *__restrict__ sft, int8_t *__restrict__ out, size_t plane,
                                             size_t ksteps, size_t kblk, size_t vmax, int flags, const ModParams &MP,
-                                            const ModGroups &G, unsigned bx, unsigned by, EncTile<R, CPLX> &tile) {
+                                            const ModGroups &G, unsigned bx, unsigned by, EncTile<R, CPLX> &tile,
+                                            const AccShift *acc = nullptr) {
     constexpr int KT = CPLX ? 32 : 64;
     constexpr int NT = CPLX ? 128 : 256;
     constexpr int NC = CPLX ? 2 : 1;
@@ -731,7 +744,15 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
 
     // this thread's vector's shift, loaded with the tile (after the barrier it cost one more memory round trip)
     const size_t vs = v0 + (tid & 63);
-    const int16_t sraw = vs < nvec ? sft[vs] : int16_t(0);
+    int16_t sraw = 0;
+    if constexpr (ACC) {
+        if (vs < nvec) {
+            sraw = accurate_sft(acc->sft0[vs], acc->bound[vs], acc->log2M);
+            if (e0 == 0 && tid < 64) acc->out[vs] = sraw;
+        }
+    } else {
+        sraw = vs < nvec ? sft[vs] : int16_t(0);
+    }
     // stage the tile, coalesced along whichever index is contiguous in HBM; interior tiles
     // load without per-element guards so all loads are in flight at once
     constexpr int NL = (64 * KT) / NT;
@@ -1088,21 +1109,23 @@ struct EncOperand {
     size_t plane, vmax;
     int flags;
     unsigned gx, gy;
+    AccShift acc;  // ACC launches: where the shifts come from (sft is then unused)
 };
-template <typename R, bool CPLX, bool CONTIG_A, bool CONTIG_B, bool NTL>
+template <typename R, bool CPLX, bool CONTIG_A, bool CONTIG_B, bool NTL, bool ACC = false>
 __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_pair_kernel(EncOperand a, EncOperand b, size_t ksteps,
                                                                         size_t kblk, ModParams MP, ModGroups G) {
     __shared__ EncTile<R, CPLX> tile;
     const unsigned na = a.gx * a.gy;
     if (MP.zero_queue && blockIdx.x == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
     if (blockIdx.x < na) {
-        encode_body<R, CPLX, CONTIG_A, true, 0, NTL>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.sft, a.out, a.plane,
-                                                ksteps, kblk, a.vmax, a.flags, MP, G, blockIdx.x % a.gx, blockIdx.x / a.gx,
-                                                tile);
+        encode_body<R, CPLX, CONTIG_A, true, 0, NTL, ACC>(static_cast<const R *>(a.X), a.ld, a.nvec, a.len, a.sft, a.out,
+                                                          a.plane, ksteps, kblk, a.vmax, a.flags, MP, G,
+                                                          blockIdx.x % a.gx, blockIdx.x / a.gx, tile, &a.acc);
     } else {
         const unsigned t = blockIdx.x - na;
-        encode_body<R, CPLX, CONTIG_B, false, 0, NTL>(static_cast<const R *>(b.X), b.ld, b.nvec, b.len, b.sft, b.out, b.plane,
-                                                 ksteps, kblk, b.vmax, b.flags, MP, G, t % b.gx, t / b.gx, tile);
+        encode_body<R, CPLX, CONTIG_B, false, 0, NTL, ACC>(static_cast<const R *>(b.X), b.ld, b.nvec, b.len, b.sft, b.out,
+                                                           b.plane, ksteps, kblk, b.vmax, b.flags, MP, G, t % b.gx,
+                                                           t / b.gx, tile, &b.acc);
     }
 }
 
@@ -1251,8 +1274,7 @@ __global__ void finalize_accurate_sft_kernel(const int16_t *__restrict__ sft0, c
     const size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= nvec) return;
     const int amax = cplx_rows ? max(bound[v], bound[v + nvec]) : bound[v];
-    const int s = sft0_stored(sft0[v]) + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
-    sft_out[v] = (int16_t)(-s);
+    sft_out[v] = accurate_sft(sft0[v], amax, log2M);
 }
 
 // both operands: vectors [0, nA) of A (sft0A, boundA), then [0, nB) of B
@@ -1264,9 +1286,7 @@ __global__ void finalize_accurate_pair_kernel(const int16_t *__restrict__ sft0A,
     const bool isA = v < nA;
     if (!isA) v -= nA;
     if (!isA && v >= nB) return;
-    const int amax = (isA ? boundA : boundB)[v];
-    const int s = sft0_stored((isA ? sft0A : sft0B)[v]) + __float2int_rd(__fmaf_rd(-0.51F, __log2f(__int2float_rn(amax)), log2M));
-    (isA ? outA : outB)[v] = (int16_t)(-s);
+    (isA ? outA : outB)[v] = accurate_sft((isA ? sft0A : sft0B)[v], (isA ? boundA : boundB)[v], log2M);
 }
 
 // zeroes the accurate-mode bound maxima before the bound product (a kernel rather than
@@ -1539,6 +1559,12 @@ static void launch_encode_pair(const EncOperand &a, const EncOperand &b, const L
                                hipStream_t st) {
     const ModGroups G = make_groups(MP, L.N);
     const dim3 grid(a.gx * a.gy + b.gx * b.gy), block(CPLX ? 128 : 256);
+    if constexpr (!CPLX) {
+        if (a.acc.sft0) {  // accurate shifts in the encode (small problems: plain loads)
+            launch(encode_pair_kernel<R, CPLX, CA, CB, false, true>, grid, block, st, a, b, L.ksteps, L.kblk, MP, G);
+            return;
+        }
+    }
     // non-temporal loads only for the real f64 form, the one large calls take (the others fork per operand)
     if (!CPLX && sizeof(R) == 8 && (a.nvec + b.nvec) * a.len * sizeof(R) >= 2 * NT_OPERAND_BYTES)
         launch(encode_pair_kernel<R, CPLX, CA, CB, !CPLX && sizeof(R) == 8>, grid, block, st, a, b, L.ksteps, L.kblk, MP, G);
@@ -1554,9 +1580,10 @@ static void launch_encode_pair_ops(bool ca, bool cb, const EncOperand &a, const 
 
 bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
                        const int16_t *sftA, const int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
-                       const ModParams &MP, hipStream_t st) {
+                       const ModParams &MP, hipStream_t st, const AccurateShifts *accs) {
     // operands of one element type (the same ModGroups and tile type); anything else: two launches
     if (dA.cplx != dB.cplx || dA.dbl != dB.dbl || L.kblk == 0) return false;
+    if (accs && (dA.cplx || L.kara)) return false;  // (real operands only: complex A rows take two bound maxima)
     const bool cplx = dA.cplx;
     const int KT = cplx ? 32 : 64;
     // per operand exactly what split_encode sets up for mode 0
@@ -1578,8 +1605,12 @@ bool split_encode_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, s
         e.gy = d.contig ? (unsigned)(vpad / 64) : (unsigned)(L.kblk / KT);
         return e;
     };
-    const EncOperand a = operand(dA, true, m, sftA, outA, L.planeA);
-    const EncOperand b = operand(dB, false, n, sftB, outB, L.planeB);
+    EncOperand a = operand(dA, true, m, sftA, outA, L.planeA);
+    EncOperand b = operand(dB, false, n, sftB, outB, L.planeB);
+    if (accs) {
+        a.acc = AccShift{accs->sft0A, accs->boundA, const_cast<int16_t *>(sftA), accs->log2M};
+        b.acc = AccShift{accs->sft0B, accs->boundB, const_cast<int16_t *>(sftB), accs->log2M};
+    }
     if (a.gx * a.gy == 0 || b.gx * b.gy == 0) return false;
     if (dA.dbl) {
         if (cplx) launch_encode_pair_ops<double, true>(dA.contig, dB.contig, a, b, L, MP, st);

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIJACK = os.path.join(ROOT, "mixed-gemmul8_amd", "gemmul8", "libgemmul8_hijack.so")
-# the tests below run small shapes: the interposer's default thresholds (1536) would forward them
+# the tests below run small shapes: the interposer's default thresholds (1280) would forward them
 SMALL_THRESHOLDS = {"GEMMUL8_INTERCEPT_THRESHOLD_M": "128", "GEMMUL8_INTERCEPT_THRESHOLD_N": "128",
                     "GEMMUL8_INTERCEPT_THRESHOLD_K": "128"}
 
@@ -340,7 +340,7 @@ print("RESULT " + json.dumps(out))
 
 
 def test_default_thresholds_follow_the_crossover():
-    """with no threshold set, DGEMMs below the measured MI355X crossover (1536) keep the vendor routine
+    """with no threshold set, DGEMMs below the measured MI355X crossover (1280) keep the vendor routine
     (512^3, 1024^3) and larger ones are emulated (2048^3, bit for bit)"""
     assert os.path.exists(HIJACK), "libgemmul8_hijack.so not built"
     env = {k: v for k, v in os.environ.items() if not k.startswith("GEMMUL8_INTERCEPT_THRESHOLD")}

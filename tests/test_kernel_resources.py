@@ -22,12 +22,14 @@ FLOORS = {
     "oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>": 2,  # the block-epilogue form (GEMMUL8_PG_EPILOGUE=0)
     "oz2::gemm_i8_small_kernel<0, false>": 2,       # small launches: 256 threads, 64 KiB LDS, 2 blocks per CU
     "oz2::gemm_i8_small_kernel<1, false>": 2,       # the accurate-mode bound product of small problems
-    "oz2::crt_kernel<0, false, 14u, false, 8, false>": 5,    # cfg2/3 CRT below n = 4096
-    "oz2::crt_kernel<0, false, 14u, false, 8, true>": 4,     # cfg2/3 CRT (4 columns per block, prefetch)
+    "oz2::crt_kernel<0, false, 14u, false, 4, false>": 5,    # cfg2/3 CRT (4 rows per lane, the default)
+    "oz2::crt_kernel<0, false, 14u, false, 8, false>": 5,    # GEMMUL8_CRT_ROWS=8
+    "oz2::crt_kernel<0, false, 14u, false, 8, true>": 4,     # ... with 4 columns per block and prefetch
     "oz2::crt_kernel<0, false, 10u, false, 8, false>": 5,    # cfg4 CRT
     "oz2::crt_kernel<2, false, 12u, true, 8, false>": 3,     # cfg5 CRT (Karatsuba residues)
     "oz2::stats_pair_kernel<16, true>": 8,             # cfg2 shifts
-    "oz2::encode_pair_kernel<double, false, false, true, true>": 4,  # cfg2 slices
+    "oz2::encode_pair_kernel<double, false, false, true, true, false>": 4,  # cfg2 slices
+    "oz2::split_fused_kernel<1024, 4, 256, false, true, false>": 4,  # small problems: shifts and slices at once
     "oz2::encode_kernel<double, true, false, false, 0, true>": 2,    # cfg5 slices
 }
 
@@ -67,14 +69,16 @@ def test_hot_kernel_occupancy(table, prefix):
         assert v["occupancy"] >= FLOORS[prefix], (n, v)
 
 
-@pytest.mark.parametrize("prefix,loads,stores", [
-    ("oz2::gemm_i8_persistent_pg_kernel<false, 1, 0>(", 0, 8),  # residue stores (LDS-DMA loads are buffer ops)
-    ("oz2::gemm_i8_persistent_pg_kernel<true, 1, 0>(", 0, 8),
-    ("oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>(", 0, 8),
-    ("oz2::crt_kernel<0, false, 14u, false, 8, false>(", 14, 4),     # 14 residue planes, C stored in 16-byte vectors
-    ("oz2::crt_kernel<2, false, 12u, true, 8, false>(", 36, 8),      # 3 Karatsuba sub-planes x 12 moduli
+@pytest.mark.parametrize("prefix,loads,stores,load_op", [
+    ("oz2::gemm_i8_persistent_pg_kernel<false, 1, 0>(", 0, 8, "dwordx2"),  # residue stores (LDS-DMA loads: buffer ops)
+    ("oz2::gemm_i8_persistent_pg_kernel<true, 1, 0>(", 0, 8, "dwordx2"),
+    ("oz2::gemm_i8_persistent_kernel<false, 1, 0, 0>(", 0, 8, "dwordx2"),
+    ("oz2::crt_kernel<0, false, 14u, false, 4, false>(", 14, 2, "dword"),  # 14 residue planes (4 rows: one dword
+                                                                            # each), C stored in 16-byte vectors
+    ("oz2::crt_kernel<0, false, 14u, false, 8, false>(", 14, 4, "dwordx2"),
+    ("oz2::crt_kernel<2, false, 12u, true, 8, false>(", 36, 8, "dwordx2"),  # 3 Karatsuba sub-planes x 12 moduli
 ])
-def test_streaming_memory_ops(prefix, loads, stores):
+def test_streaming_memory_ops(prefix, loads, stores, load_op):
     """the streams read or written once per call stay out of the caches (non-temporal), and the
     CRT's residue loads are global, not flat (a flat load also counts in lgkmcnt, so scalar and LDS waits would
     wait for the residues in flight)"""
@@ -83,5 +87,5 @@ def test_streaming_memory_ops(prefix, loads, stores):
     (body,) = K.disassembly(prefix)
     ops = [ln.split("//")[0] for ln in body.splitlines() if re.search(r"\s(global|flat)_(load|store)", ln)]
     assert not [o for o in ops if "flat_load_dwordx2" in o], "residue loads through flat addresses"
-    assert sum("global_load_dwordx2" in o and o.rstrip().endswith(" nt") for o in ops) == loads
+    assert sum(o.split()[0] == "global_load_" + load_op and o.rstrip().endswith(" nt") for o in ops) == loads
     assert sum("global_store_dwordx4" in o and o.rstrip().endswith(" nt") for o in ops) == stores
