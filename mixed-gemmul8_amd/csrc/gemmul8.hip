@@ -287,9 +287,11 @@ static void phase_bound(const Call &c, const Views &v, size_t c0 = 0, size_t c1 
     const size_t s1A = v.L.S >= 2 ? L.planeA : 0, s1B = v.L.S >= 2 ? L.planeB : 0;
     // one stream (small problems): both operands' magnitudes in two launches, the bound maxima zeroed by the second
     const bool pair = !c.lane && !sft0_ready && one_read_magnitudes() &&
-                      split_magnitudes_pair(c.A, c.m, c.B, c.n, c.k, v.sft0, v.sft0 + L.m_pad, v.A8, v.B8, L,
+                      (split_fused_magnitudes_pair(c.A, c.m, c.B, c.n, c.k, v.sft0, v.sft0 + L.m_pad, v.A8, v.B8, L,
+                                                   MP, v.bound, L.m_pad + L.n_pad, c.st) ||
+                       split_magnitudes_pair(c.A, c.m, c.B, c.n, c.k, v.sft0, v.sft0 + L.m_pad, v.A8, v.B8, L,
                                             v.A8 + L.planeA, s1A, v.B8 + L.planeB, s1B, v.bound, L.m_pad + L.n_pad,
-                                            c.st);
+                                            c.st));
     if (pair) {
     } else if (sft0_ready || !one_read_magnitudes() ||
         !split_magnitudes(c.A, true, c.m, c.k, v.sft0, v.A8, L, v.A8 + L.planeA, s1A, c.st)) {

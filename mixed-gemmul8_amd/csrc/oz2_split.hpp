@@ -109,6 +109,11 @@ void split_finalize_accurate_pair(const int16_t *sft0A, const int32_t *boundA, s
 bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
                       float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
                       const ModParams &MP, hipStream_t st);
+// accurate mode, one stream, real f64, k <= 2048: sft0 and the magnitude plane of both operands in one launch
+// that reads each operand once (split_fused_kernel, MAG), zeroing the bound maxima [0, nbound)
+bool split_fused_magnitudes_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
+                                 int16_t *sft0A, int16_t *sft0B, int8_t *outA, int8_t *outB, const Layout &L,
+                                 const ModParams &MP, int32_t *bound, size_t nbound, hipStream_t st);
 // accurate mode (real operands): the encode computes the final shifts itself from sft0 and the bound maxima and
 // stores them to sftA / sftB (finalize_accurate_sft_kernel's arithmetic, one launch fewer)
 struct AccurateShifts {

@@ -1155,7 +1155,8 @@ struct FusedOperand {
     int16_t *sft;
     int8_t *out;
 };
-template <int KMAX, int FZ_V, int FZ_NT, bool CONTIG, bool NTL>
+// MAG: accurate mode's first pass instead -- sft0 = 5 - ilogb(vector amax) and the 6-bit magnitude plane (MODE 1)
+template <int KMAX, int FZ_V, int FZ_NT, bool CONTIG, bool NTL, bool MAG = false>
 __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, size_t len, size_t ksteps, size_t kblk,
                                            float log2M, const ModParams &MP, const ModGroups &G, unsigned bx,
                                            double (&panel)[FZ_V][FZ_ROW<KMAX>], int (&shl)[FZ_V]) {
@@ -1201,7 +1202,21 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
         // wave w < FZ_V: vector v0 + w; lane l: the chains of virtual threads l and l + 64 (elements vt + 128 i, in
         // order)
         const int w = tid >> 6, lane = tid & 63;
-        if (w < FZ_V) {
+        if (MAG && w < FZ_V) {
+            double amax = 0;
+            for (int i = 0; i < KMAX / 64; ++i) amax = fmax(amax, fabs(panel[w][fz_idx(lane + 64 * i)]));
+            const double mx = wave_max<double>(amax);
+            const size_t v = v0 + w;
+            if (lane == 0) {
+                int sh = 0;
+                if (v < o.nvec) {
+                    const int16_t s0 = sft0_of<double>(mx);
+                    o.sft[v] = s0;
+                    sh = sft0_scale<double>(s0);
+                }
+                shl[w] = sh;
+            }
+        } else if (w < FZ_V) {
         double a0 = 0, a1 = 0, amax = 0;
         static_assert(KMAX % 512 == 0, "chains in groups of four");
         for (int i = 0; i < KMAX / 128; i += 4) {
@@ -1241,30 +1256,34 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
         double yr[16], yi[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            yr[q] = trunc(scalbn(panel[r][fz_idx((int)kk) + q], sh));
+            const double x = panel[r][fz_idx((int)kk) + q];
+            yr[q] = MAG ? scalbn(fabs(x), sh) : trunc(scalbn(x, sh));
             yi[q] = 0;
         }
-        if (is_a) encode_vec16<double, false, true, 0>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
-        else encode_vec16<double, false, false, 0>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
+        constexpr int MODE = MAG ? 1 : 0;
+        if (is_a) encode_vec16<double, false, true, MODE>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
+        else encode_vec16<double, false, false, MODE>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
     }
 }
-template <int KMAX, int FZ_V, int FZ_NT, bool CA, bool CB, bool NTL = false>
+template <int KMAX, int FZ_V, int FZ_NT, bool CA, bool CB, bool NTL = false, bool MAG = false>
 __global__ __launch_bounds__(FZ_NT) void split_fused_kernel(FusedOperand a, FusedOperand b, size_t len,
                                                             size_t ksteps, size_t kblk, float log2M, ModParams MP,
-                                                            ModGroups G) {
+                                                            ModGroups G, int32_t *zero, size_t nzero) {
     __shared__ double panel[FZ_V][FZ_ROW<KMAX>];
     __shared__ int shl[FZ_V];
     if (MP.zero_queue && blockIdx.x == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
+    // (MAG: the bound maxima the bound product accumulates into with atomicMax)
+    for (size_t i = (size_t)blockIdx.x * FZ_NT + threadIdx.x; i < nzero; i += (size_t)gridDim.x * FZ_NT) zero[i] = 0;
     const unsigned na = (unsigned)(a.vpad / FZ_V), nb = (unsigned)(b.vpad / FZ_V);
     // (na and nb are multiples of 8 (vpad of 64): a strided operand's neighbouring blocks, which share its 128-byte
     // input lines, are renumbered onto one XCD)
     if (blockIdx.x < na) {
         const unsigned bx = CA && !OZ2_FZ_XCD_CONTIG ? blockIdx.x : xcd_local_block(blockIdx.x, na);
-        fused_body<KMAX, FZ_V, FZ_NT, CA, NTL>(a, true, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+        fused_body<KMAX, FZ_V, FZ_NT, CA, NTL, MAG>(a, true, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
     } else {
         const unsigned t = blockIdx.x - na;
         const unsigned bx = CB && !OZ2_FZ_XCD_CONTIG ? t : xcd_local_block(t, nb);
-        fused_body<KMAX, FZ_V, FZ_NT, CB, NTL>(b, false, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+        fused_body<KMAX, FZ_V, FZ_NT, CB, NTL, MAG>(b, false, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
     }
 }
 
@@ -1488,11 +1507,12 @@ static int fused_split_mode() {  // GEMMUL8_FUSED_SPLIT=0: the two-launch split 
     }();
     return v;
 }
-bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
-                      float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
-                      const ModParams &MP, hipStream_t st) {
-    if (!fused_split_mode() || dA.cplx || dB.cplx || !dA.dbl || !dB.dbl || VT != 128 || L.kara || L.kblk == 0 ||
-        L.kblk > 2048 || m == 0 || n == 0)
+template <bool MAG>
+static bool fused_pair_launch(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
+                              float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
+                              const ModParams &MP, int32_t *zero, size_t nzero, hipStream_t st) {
+    if (!fused_split_mode() || dA.cplx || dB.cplx || !dA.dbl || !dB.dbl || L.kara || L.kblk == 0 || L.kblk > 2048 ||
+        m == 0 || n == 0)
         return false;
     FusedOperand a{}, b{};
     a.X = static_cast<const double *>(dA.ptr);
@@ -1520,15 +1540,26 @@ bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, si
     if (blocks > 0x7fffffff) return false;
     const ModGroups G = make_groups(MP, L.N);
     const dim3 grid((unsigned)blocks), block(64 * fv);
-#define OZ2_FZ(K, V) do { if (dA.contig) { if (dB.contig) launch(split_fused_kernel<K, V, 64 * V, true, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
-                                            else launch(split_fused_kernel<K, V, 64 * V, true, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } \
-                          else { if (dB.contig) launch(split_fused_kernel<K, V, 64 * V, false, true>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); \
-                                 else launch(split_fused_kernel<K, V, 64 * V, false, false>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G); } } while (0)
+#define OZ2_FZ1(K, V, CA, CB) launch(split_fused_kernel<K, V, 64 * V, CA, CB, false, MAG>, grid, block, st, a, b, len, L.ksteps, L.kblk, log2M, MP, G, zero, nzero)
+#define OZ2_FZ(K, V) do { if (dA.contig) { if (dB.contig) OZ2_FZ1(K, V, true, true); else OZ2_FZ1(K, V, true, false); } \
+                          else { if (dB.contig) OZ2_FZ1(K, V, false, true); else OZ2_FZ1(K, V, false, false); } } while (0)
     if (L.kblk <= 1024) { if (fv == 8) OZ2_FZ(1024, 8); else OZ2_FZ(1024, 4); }
     else if (L.kblk <= 1536) { if (fv == 8) OZ2_FZ(1536, 8); else OZ2_FZ(1536, 4); }
     else { if (fv == 8) OZ2_FZ(2048, 8); else OZ2_FZ(2048, 4); }
 #undef OZ2_FZ
+#undef OZ2_FZ1
     return true;
+}
+bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len, int VT,
+                      float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
+                      const ModParams &MP, hipStream_t st) {
+    if (VT != 128) return false;  // (the reference's VT = 128 summation order)
+    return fused_pair_launch<false>(dA, m, dB, n, len, log2M, sftA, sftB, outA, outB, L, MP, nullptr, 0, st);
+}
+bool split_fused_magnitudes_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
+                                 int16_t *sft0A, int16_t *sft0B, int8_t *outA, int8_t *outB, const Layout &L,
+                                 const ModParams &MP, int32_t *bound, size_t nbound, hipStream_t st) {
+    return fused_pair_launch<true>(dA, m, dB, n, len, 0.f, sft0A, sft0B, outA, outB, L, MP, bound, nbound, st);
 }
 
 void split_finalize_accurate_pair(const int16_t *sft0A, const int32_t *boundA, size_t m, const int16_t *sft0B,
