@@ -205,8 +205,8 @@ int gemmul8_dd_gemm(void *stream, size_t m, size_t n, size_t k, const double *A,
 /* err[i] = |C[i] - (C1[i] + C2[i])| / |C1[i] + C2[i]| evaluated in double-double (eval.hpp:317-338). */
 int gemmul8_relerr_dd(void *stream, size_t count, const double *C, const double *C1, const double *C2, double *err);
 /* the reference drivers' timing loop (GEMMul8/testing/test_double.cu:422-431) in native code: `iters` calls of
- * gemmul8_gemm, each bracketed by hipDeviceSynchronize and the host clock; *sec = mean seconds per call,
- * phase_ns[4] = mean phase times (NULL: not returned) */
+ * gemmul8_gemm, each bracketed by hipDeviceSynchronize and the host clock; *sec = mean seconds per call (calls
+ * without phase events), phase_ns[4] = mean phase times from a second loop of `iters` calls (NULL: not run) */
 int gemmul8_time_gemm(void *stream, int op_a, int op_b, size_t m, size_t n, size_t k, int type_a, int type_b,
                       int type_c, const void *alpha, const void *A, size_t lda, const void *B, size_t ldb,
                       const void *beta, void *C, size_t ldc, unsigned num_moduli, int fastmode, void *work,
