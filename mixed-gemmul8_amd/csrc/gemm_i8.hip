@@ -1411,9 +1411,19 @@ static int persistent_mode() {
     return env;
 }
 
+// GEMMUL8_TAIL_SMALL=1 (read once): 128 x 128 tail planes (below; measured slower, so off by default)
+static bool tail_small_mode() {
+    static const bool on = [] {
+        const char *e = getenv("GEMMUL8_TAIL_SMALL");
+        return e ? atoi(e) != 0 : false;
+    }();
+    return on;
+}
+std::atomic<int> g_last_tail_small{0};
+
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
              int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue,
-             bool queue_zeroed) {
+             bool queue_zeroed, bool tail_small) {
     GemmArgs g{};
     g.A = A8;
     g.B = B8;
@@ -1487,8 +1497,40 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
     // (residue and bound products over buffer descriptors), unset by that rule unless GEMMUL8_PERSISTENT forces
     // a 256-tile kernel.
     const int smode = small_tiles_mode();
+    // Tail planes (GEMMUL8_TAIL_SMALL=1): a residue launch whose last round of 256 x 256 tiles would leave CUs idle
+    // (2048^3: 896 tiles, 3.5 per CU; 1152^3: 350 on 256 CUs) runs the planes that fit one round fewer on the
+    // 256-tile kernels and the rest, at most half a round of 256-tiles, as 128 x 128 tiles (two blocks per CU: one
+    // round of them).  Same residues (integer sums), but slower: 2048^3 products 98.5-99.1 -> 102.7-104.0 us, 1152^3
+    // 36.5-36.9 -> 38.0-38.3 us (profiles/r06/mid_sizes/tail_small_ab.txt): the 128 x 128 round costs more than the
+    // half-empty 256-tile round it replaces.
+    if (epi == Epi::RESIDUE && !tail_small && g.nsub == 1 && buf && smode == 2 && pmode == 2 && tail_small_mode()) {
+        const unsigned T = (unsigned)(L.mtiles * L.ntiles);
+        const unsigned rounds = (ntiles_all + ncu - 1) / ncu;
+        if (rounds >= 2 && ntiles_all % ncu != 0) {
+            const unsigned keep = (unsigned)(((size_t)(rounds - 1) * ncu) / T);
+            const unsigned tail = nplanes - keep;
+            if (keep >= 1 && tail >= 1 && 2 * (size_t)tail * T <= ncu) {
+                gemm_i8(A8, B8, L, keep, epi, out, rowmax, colmax, MP, st, queue, queue_zeroed, false);
+                const int head = g_last_residue_kernel.load(std::memory_order_relaxed);
+                ModParams M2 = MP;
+                for (unsigned i = 0; i < tail; ++i) {
+                    M2.p[i] = MP.p[keep + i];
+                    M2.barrett[i] = MP.barrett[keep + i];
+                    M2.rinv_d[i] = MP.rinv_d[keep + i];
+                    M2.rinv_f[i] = MP.rinv_f[keep + i];
+                }
+                M2.N = tail;
+                gemm_i8(A8 + keep * L.planeA, B8 + keep * L.planeB, L, tail, epi,
+                        static_cast<uint8_t *>(out) + keep * L.planeR, nullptr, nullptr, M2, st, nullptr, true, true);
+                g_last_residue_kernel.store(head, std::memory_order_relaxed);
+                g_last_tail_small.store(1, std::memory_order_relaxed);
+                return;
+            }
+        }
+    }
+    if (epi == Epi::RESIDUE && !tail_small) g_last_tail_small.store(0, std::memory_order_relaxed);
     if ((epi == Epi::RESIDUE || epi == Epi::BOUND) && buf &&
-        (smode == 1 || (smode == 2 && pmode == 2 && epi == Epi::BOUND && ntiles_all < ncu))) {
+        (smode == 1 || tail_small || (smode == 2 && pmode == 2 && epi == Epi::BOUND && ntiles_all < ncu))) {
         const dim3 sgrid((unsigned)(4 * L.mtiles * L.ntiles), nplanes * g.nsub);
         if (epi == Epi::RESIDUE) {
             g_last_residue_kernel.store(4, std::memory_order_relaxed);

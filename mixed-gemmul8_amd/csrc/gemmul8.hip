@@ -850,12 +850,13 @@ int gemmul8_set_epilogue(int mode) {
 int gemmul8_get_epilogue(void) { return oz2::g_epilogue_mode.load(std::memory_order_relaxed); }
 
 const char *gemmul8_last_products_kernel(void) {
+    const bool tail = oz2::g_last_tail_small.load(std::memory_order_relaxed) != 0;
     switch (oz2::g_last_residue_kernel.load(std::memory_order_relaxed)) {
-    case 1: return "gemm_i8_kernel";
-    case 2: return "gemm_i8_persistent_kernel";
+    case 1: return tail ? "gemm_i8_kernel+gemm_i8_small_kernel" : "gemm_i8_kernel";
+    case 2: return tail ? "gemm_i8_persistent_kernel+gemm_i8_small_kernel" : "gemm_i8_persistent_kernel";
     case 3: return "gemm_i8_kernel (k-chunked)";
     case 4: return "gemm_i8_small_kernel";
-    case 5: return "gemm_i8_persistent_pg_kernel";
+    case 5: return tail ? "gemm_i8_persistent_pg_kernel+gemm_i8_small_kernel" : "gemm_i8_persistent_pg_kernel";
     default: return "none";
     }
 }

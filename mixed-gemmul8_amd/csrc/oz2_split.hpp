@@ -137,12 +137,15 @@ enum class Epi : int { RESIDUE = 0, BOUND = 1, RAW = 2 };
 // queue: the workspace's tile-queue area (Layout::offQueue) for the persistent residue kernel
 // (nullptr: one-tile kernel only); queue_zeroed: an earlier launch on st zeroed it (else a zeroing
 // launch precedes the persistent kernel).
+// tail_small: this launch is the 128 x 128 tail of a residue launch (gemm_i8 splits it off itself)
 void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplanes, Epi epi, void *out,
              int32_t *rowmax, int32_t *colmax, const ModParams &MP, hipStream_t st, uint32_t *queue = nullptr,
-             bool queue_zeroed = false);
+             bool queue_zeroed = false, bool tail_small = false);
 // the residue-product kernel of the last RESIDUE launch: 0 none yet, 1 one-tile (gemm_i8_kernel),
-// 2 persistent (gemm_i8_persistent_kernel), 3 k-chunked one-tile launches
+// 2 persistent (gemm_i8_persistent_kernel), 3 k-chunked one-tile launches, 4 128 x 128 (gemm_i8_small_kernel),
+// 5 persistent per-group (gemm_i8_persistent_pg_kernel); g_last_tail_small: its last planes ran as 128 x 128 tiles
 extern std::atomic<int> g_last_residue_kernel;
+extern std::atomic<int> g_last_tail_small;
 // exhaustive exactness check of the residue epilogues (0 = biased, 1 = signed): mismatch count
 unsigned long long residue_selftest(int path, hipStream_t st);
 

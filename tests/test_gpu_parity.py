@@ -800,7 +800,8 @@ def test_small_tiles_match_one_tile():
             "cases = ((1024, 1024, 1024, 14, True, 'd', 0), (300, 200, 64, 14, True, 'd', 0),\n"
             "         (900, 130, 2100, 14, True, 'd', 0), (1024, 1024, 1024, 14, False, 'd', 0),\n"
             "         (700, 540, 333, 9, False, 'd', 0), (520, 270, 400, 7, True, 'f', 0),\n"
-            "         (1024, 300, 3072, 12, True, 'z', 3), (2048, 2048, 2048, 14, True, 'd', 0))\n"
+            "         (1024, 300, 3072, 12, True, 'z', 3), (2048, 2048, 2048, 14, True, 'd', 0),\n"
+            "         (1152, 1152, 1152, 14, True, 'd', 0), (1152, 1152, 1152, 14, False, 'd', 0))\n"
             "for m, n, k, N, fast, t, ct in cases:\n"
             "    dt = {'d': torch.float64, 'f': torch.float32, 'z': torch.complex128}[t]\n"
             "    g = torch.Generator(device='cuda'); g.manual_seed(m + n + k)\n"
@@ -813,12 +814,13 @@ def test_small_tiles_match_one_tile():
             "    res[f'{m}_{n}_{k}_{N}_{fast}_{t}_kernel'] = np.array([G.last_products_kernel()])\n"
             "np.savez(out, **res)\n")
     modes = {"onetile": {"GEMMUL8_SMALL_TILES": "0", "GEMMUL8_PERSISTENT": "0"}, "default": {},
-             "forced": {"GEMMUL8_SMALL_TILES": "1"}}
+             "forced": {"GEMMUL8_SMALL_TILES": "1"}, "tail": {"GEMMUL8_TAIL_SMALL": "1"}}
     with tempfile.TemporaryDirectory() as d:
         outs = {}
         for name, extra in modes.items():
             out = os.path.join(d, f"{name}.npz")
-            env = {kk: v for kk, v in os.environ.items() if kk not in ("GEMMUL8_SMALL_TILES", "GEMMUL8_PERSISTENT")}
+            env = {kk: v for kk, v in os.environ.items()
+                   if kk not in ("GEMMUL8_SMALL_TILES", "GEMMUL8_PERSISTENT", "GEMMUL8_TAIL_SMALL")}
             env.update(extra)
             r = subprocess.run([sys.executable, "-c", code, os.path.join(root, "mixed-gemmul8_amd"), tdir, out],
                                env=env, capture_output=True, text=True, timeout=300)
@@ -827,12 +829,17 @@ def test_small_tiles_match_one_tile():
         for key in outs["onetile"].files:
             if key.endswith("_kernel"):
                 continue
-            for name in ("default", "forced"):
+            for name in ("default", "forced", "tail"):
                 assert np.array_equal(outs["onetile"][key].view(np.uint8), outs[name][key].view(np.uint8)), (name, key)
         assert str(outs["forced"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
         assert str(outs["forced"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
         assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
         assert str(outs["default"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_persistent_pg_kernel"
+        # tail planes: 2048^3 (3.5 tiles per CU) 12 planes on the persistent kernel (3 rounds), the last 2 as
+        # 128 x 128 tiles; 1152^3 (350 tiles on 256 CUs) 10 planes on the one-tile kernel and 4 as 128 x 128 tiles
+        assert str(outs["tail"]["2048_2048_2048_14_True_d_kernel"][0]) == \
+            "gemm_i8_persistent_pg_kernel+gemm_i8_small_kernel"
+        assert str(outs["tail"]["1152_1152_1152_14_True_d_kernel"][0]) == "gemm_i8_kernel+gemm_i8_small_kernel"
         assert str(outs["onetile"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
     code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
             "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
