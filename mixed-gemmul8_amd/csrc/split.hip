@@ -1156,37 +1156,28 @@ struct FusedOperand {
     int8_t *out;
 };
 // MAG: accurate mode's first pass instead -- sft0 = 5 - ilogb(vector amax) and the 6-bit magnitude plane (MODE 1)
-template <int KMAX, int FZ_V, int FZ_NT, bool CONTIG, bool NTL, bool MAG = false>
-__device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, size_t len, size_t ksteps, size_t kblk,
-                                           float log2M, const ModParams &MP, const ModGroups &G, unsigned bx,
-                                           double (&panel)[FZ_V][FZ_ROW<KMAX>], int (&shl)[FZ_V]) {
-    static_assert(KMAX % 128 == 0 && KMAX % FZ_NT == 0 && FZ_NT >= 64 * FZ_V, "whole chains and load rounds");
+// the loads of vectors [v0, v0 + FZ_V) into registers (zeros past len and past nvec): KMAX / 64 per thread
+template <int KMAX, int FZ_V, int FZ_NT, bool CONTIG, bool NTL>
+__device__ __forceinline__ void fz_load(const FusedOperand &o, size_t len, size_t v0, double (&x)[KMAX / 64]) {
+    static_assert(KMAX % 128 == 0 && KMAX % FZ_NT == 0 && FZ_NT == 64 * FZ_V, "whole chains and load rounds");
     const int tid = threadIdx.x;
-    const size_t v0 = (size_t)bx * FZ_V;
-    // stage the vectors: zeros past len and past nvec
     if (CONTIG) {
         // vector j's elements e = tid + FZ_NT i: each wave load is 512 contiguous bytes
         constexpr int PER = KMAX / FZ_NT;
 #pragma unroll
-        for (int j = 0; j < FZ_V; ++j) {
-            double x[PER > 0 ? PER : 1];
-            const size_t v = v0 + j;
+        for (int j = 0; j < FZ_V; ++j)
 #pragma unroll
             for (int i = 0; i < PER; ++i) {
-                const size_t e = tid + (size_t)FZ_NT * i;
+                const size_t v = v0 + j, e = tid + (size_t)FZ_NT * i;
                 double im;
-                x[i] = 0.0;
-                if (v < o.nvec && e < len) load_elem<double, false, NTL>(o.X, v * o.ld + e, x[i], im);
+                x[j * PER + i] = 0.0;
+                if (v < o.nvec && e < len) load_elem<double, false, NTL>(o.X, v * o.ld + e, x[j * PER + i], im);
             }
-#pragma unroll
-            for (int i = 0; i < PER; ++i) panel[j][fz_idx(tid + FZ_NT * i)] = x[i];
-        }
     } else {
         // row r = tid mod FZ_V of column e = tid / FZ_V + 64 i: 8 FZ_V contiguous bytes per column
         constexpr int PER = KMAX / (FZ_NT / FZ_V);
         const int r = tid & (FZ_V - 1), c = tid / FZ_V;
         const size_t v = v0 + r;
-        double x[PER];
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const size_t e = c + (size_t)(FZ_NT / FZ_V) * i;
@@ -1194,10 +1185,31 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
             x[i] = 0.0;
             if (v < o.nvec && e < len) load_elem<double, false, NTL>(o.X, e * o.ld + v, x[i], im);
         }
+    }
+}
+template <int KMAX, int FZ_V, int FZ_NT, bool CONTIG>
+__device__ __forceinline__ void fz_stage(const double (&x)[KMAX / 64], double (&panel)[FZ_V][FZ_ROW<KMAX>]) {
+    const int tid = threadIdx.x;
+    if (CONTIG) {
+        constexpr int PER = KMAX / FZ_NT;
+#pragma unroll
+        for (int j = 0; j < FZ_V; ++j)
+#pragma unroll
+            for (int i = 0; i < PER; ++i) panel[j][fz_idx(tid + FZ_NT * i)] = x[j * PER + i];
+    } else {
+        constexpr int PER = KMAX / (FZ_NT / FZ_V);
+        const int r = tid & (FZ_V - 1), c = tid / FZ_V;
 #pragma unroll
         for (int i = 0; i < PER; ++i) panel[r][fz_idx(c + (FZ_NT / FZ_V) * i)] = x[i];
     }
-    __syncthreads();
+}
+// shifts and slices of the staged vectors [v0, v0 + FZ_V) (the panel filled and synchronised); ends with the panel
+// still being read (the caller synchronises before restaging it)
+template <int KMAX, int FZ_V, int FZ_NT, bool MAG = false>
+__device__ __forceinline__ void fz_compute(const FusedOperand &o, bool is_a, size_t len, size_t ksteps, size_t kblk,
+                                           float log2M, const ModParams &MP, const ModGroups &G, size_t v0,
+                                           double (&panel)[FZ_V][FZ_ROW<KMAX>], int (&shl)[FZ_V]) {
+    const int tid = threadIdx.x;
     {
         // wave w < FZ_V: vector v0 + w; lane l: the chains of virtual threads l and l + 64 (elements vt + 128 i, in
         // order)
@@ -1217,34 +1229,34 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
                 shl[w] = sh;
             }
         } else if (w < FZ_V) {
-        double a0 = 0, a1 = 0, amax = 0;
-        static_assert(KMAX % 512 == 0, "chains in groups of four");
-        for (int i = 0; i < KMAX / 128; i += 4) {
-            double x0[4], x1[4];
+            double a0 = 0, a1 = 0, amax = 0;
+            static_assert(KMAX % 512 == 0, "chains in groups of four");
+            for (int i = 0; i < KMAX / 128; i += 4) {
+                double x0[4], x1[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                x0[u] = fabs(panel[w][fz_idx(lane + 128 * (i + u))]);
-                x1[u] = fabs(panel[w][fz_idx(lane + 64 + 128 * (i + u))]);
-                amax = fmax(amax, fmax(x0[u], x1[u]));
+                for (int u = 0; u < 4; ++u) {
+                    x0[u] = fabs(panel[w][fz_idx(lane + 128 * (i + u))]);
+                    x1[u] = fabs(panel[w][fz_idx(lane + 64 + 128 * (i + u))]);
+                    amax = fmax(amax, fmax(x0[u], x1[u]));
+                }
+                sq_add4x2_ru(x0, x1, a0, a1);
             }
-            sq_add4x2_ru(x0, x1, a0, a1);
-        }
-        const double mx = wave_max<double>(amax);
-        const double s0 = ref_wave_sum<double>(a0), s1 = ref_wave_sum<double>(a1);
-        const double g00 = __shfl(s0, 1), g01 = __shfl(s0, 33), g10 = __shfl(s1, 1), g11 = __shfl(s1, 33);
-        double gv = lane == 32 ? g00 : lane == 33 ? g01 : lane == 34 ? g10 : lane == 35 ? g11 : 0.0;
-        gv = ref_wave_sum<double>(gv);
-        const double nrm = __shfl(gv, 32);
-        const size_t v = v0 + w;
-        if (lane == 0) {
-            int sh = 0;
-            if (v < o.nvec) {
-                const int16_t st = (int16_t)(-compute_sft(mx, nrm, log2M));
-                o.sft[v] = st;
-                sh = -(int)st;
+            const double mx = wave_max<double>(amax);
+            const double s0 = ref_wave_sum<double>(a0), s1 = ref_wave_sum<double>(a1);
+            const double g00 = __shfl(s0, 1), g01 = __shfl(s0, 33), g10 = __shfl(s1, 1), g11 = __shfl(s1, 33);
+            double gv = lane == 32 ? g00 : lane == 33 ? g01 : lane == 34 ? g10 : lane == 35 ? g11 : 0.0;
+            gv = ref_wave_sum<double>(gv);
+            const double nrm = __shfl(gv, 32);
+            const size_t v = v0 + w;
+            if (lane == 0) {
+                int sh = 0;
+                if (v < o.nvec) {
+                    const int16_t st = (int16_t)(-compute_sft(mx, nrm, log2M));
+                    o.sft[v] = st;
+                    sh = -(int)st;
+                }
+                shl[w] = sh;
             }
-            shl[w] = sh;
-        }
         }
     }
     __syncthreads();
@@ -1265,7 +1277,29 @@ __device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, siz
         else encode_vec16<double, false, false, MODE>(yr, yi, v, kk, o.nvec, len, o.out, o.plane, ksteps, kblk, o.vmax, 0, MP, G);
     }
 }
-template <int KMAX, int FZ_V, int FZ_NT, bool CA, bool CB, bool NTL = false, bool MAG = false>
+// GRP groups of FZ_V vectors per block, software-pipelined: the next group's loads are in flight (registers) while
+// the current group is summed and encoded from LDS
+template <int KMAX, int FZ_V, int FZ_NT, bool CONTIG, bool NTL, bool MAG, int GRP>
+__device__ __forceinline__ void fused_body(const FusedOperand &o, bool is_a, size_t len, size_t ksteps, size_t kblk,
+                                           float log2M, const ModParams &MP, const ModGroups &G, unsigned bx,
+                                           double (&panel)[FZ_V][FZ_ROW<KMAX>], int (&shl)[FZ_V]) {
+    double x[KMAX / 64];
+    const size_t vb = (size_t)bx * FZ_V * GRP;
+    fz_load<KMAX, FZ_V, FZ_NT, CONTIG, NTL>(o, len, vb, x);
+    fz_stage<KMAX, FZ_V, FZ_NT, CONTIG>(x, panel);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < GRP; ++t) {
+        if (t + 1 < GRP) fz_load<KMAX, FZ_V, FZ_NT, CONTIG, NTL>(o, len, vb + (size_t)(t + 1) * FZ_V, x);
+        fz_compute<KMAX, FZ_V, FZ_NT, MAG>(o, is_a, len, ksteps, kblk, log2M, MP, G, vb + (size_t)t * FZ_V, panel, shl);
+        if (t + 1 < GRP) {
+            __syncthreads();
+            fz_stage<KMAX, FZ_V, FZ_NT, CONTIG>(x, panel);
+            __syncthreads();
+        }
+    }
+}
+template <int KMAX, int FZ_V, int FZ_NT, bool CA, bool CB, bool NTL = false, bool MAG = false, int GRP = 1>
 __global__ __launch_bounds__(FZ_NT) void split_fused_kernel(FusedOperand a, FusedOperand b, size_t len,
                                                             size_t ksteps, size_t kblk, float log2M, ModParams MP,
                                                             ModGroups G, int32_t *zero, size_t nzero) {
@@ -1274,16 +1308,15 @@ __global__ __launch_bounds__(FZ_NT) void split_fused_kernel(FusedOperand a, Fuse
     if (MP.zero_queue && blockIdx.x == 0 && threadIdx.x < 8) MP.zero_queue[threadIdx.x] = 0;
     // (MAG: the bound maxima the bound product accumulates into with atomicMax)
     for (size_t i = (size_t)blockIdx.x * FZ_NT + threadIdx.x; i < nzero; i += (size_t)gridDim.x * FZ_NT) zero[i] = 0;
-    const unsigned na = (unsigned)(a.vpad / FZ_V), nb = (unsigned)(b.vpad / FZ_V);
-    // (na and nb are multiples of 8 (vpad of 64): a strided operand's neighbouring blocks, which share its 128-byte
-    // input lines, are renumbered onto one XCD)
+    const unsigned na = (unsigned)(a.vpad / (FZ_V * GRP)), nb = (unsigned)(b.vpad / (FZ_V * GRP));
+    // (a strided operand's neighbouring blocks, which share its 128-byte input lines, are renumbered onto one XCD)
     if (blockIdx.x < na) {
         const unsigned bx = CA && !OZ2_FZ_XCD_CONTIG ? blockIdx.x : xcd_local_block(blockIdx.x, na);
-        fused_body<KMAX, FZ_V, FZ_NT, CA, NTL, MAG>(a, true, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+        fused_body<KMAX, FZ_V, FZ_NT, CA, NTL, MAG, GRP>(a, true, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
     } else {
         const unsigned t = blockIdx.x - na;
         const unsigned bx = CB && !OZ2_FZ_XCD_CONTIG ? t : xcd_local_block(t, nb);
-        fused_body<KMAX, FZ_V, FZ_NT, CB, NTL, MAG>(b, false, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
+        fused_body<KMAX, FZ_V, FZ_NT, CB, NTL, MAG, GRP>(b, false, len, ksteps, kblk, log2M, MP, G, bx, panel, shl);
     }
 }
 
@@ -1531,7 +1564,8 @@ static bool fused_pair_launch(const OperandDesc &dA, size_t m, const OperandDesc
     b.vmax = L.n_pad;
     b.sft = sftB;
     b.out = outB;
-    // vectors per block: GEMMUL8_FUSED_V = 4 / 8 (read once), by default 4
+    // vectors per block: GEMMUL8_FUSED_V = 4 / 8 (read once), by default 4.  (Two or four pipelined groups of 4 per
+    // block, GRP in fused_body, measured 1.3-1.9x slower: fewer blocks, fewer waves; fused_split/grp_ab.txt.)
     static const int fv = [] {
         const char *e = getenv("GEMMUL8_FUSED_V");
         return e && atoi(e) == 8 ? 8 : 4;
