@@ -29,7 +29,7 @@ FLOORS = {
     "oz2::crt_kernel<2, false, 12u, true, 8, false>": 3,     # cfg5 CRT (Karatsuba residues)
     "oz2::stats_pair_kernel<16, true>": 8,             # cfg2 shifts
     "oz2::encode_pair_kernel<double, false, false, true, true, false>": 4,  # cfg2 slices
-    "oz2::split_fused_kernel<1024, 4, 256, false, true, false, false>": 4,  # small problems: shifts and slices at once
+    "oz2::split_fused_kernel<1024, 4, 256, false, true, false, false, 1>": 4,  # small problems: shifts and slices at once
     "oz2::encode_kernel<double, true, false, false, 0, true>": 2,    # cfg5 slices
 }
 
