@@ -110,7 +110,8 @@ bool split_fused_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, si
                       float log2M, int16_t *sftA, int16_t *sftB, int8_t *outA, int8_t *outB, const Layout &L,
                       const ModParams &MP, hipStream_t st);
 // accurate mode, one stream, real f64, k <= 2048: sft0 and the magnitude plane of both operands in one launch
-// that reads each operand once (split_fused_kernel, MAG), zeroing the bound maxima [0, nbound)
+// that reads each operand once (split_fused_kernel, MAG), zeroing the bound maxima [0, nbound); false (nothing
+// launched) where it does not apply (GEMMUL8_FUSED_SPLIT=0: never)
 bool split_fused_magnitudes_pair(const OperandDesc &dA, size_t m, const OperandDesc &dB, size_t n, size_t len,
                                  int16_t *sft0A, int16_t *sft0B, int8_t *outA, int8_t *outB, const Layout &L,
                                  const ModParams &MP, int32_t *bound, size_t nbound, hipStream_t st);
