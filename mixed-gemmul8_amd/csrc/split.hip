@@ -711,7 +711,15 @@ __device__ __forceinline__ void encode_vec16(const R (&yr)[16], const R (&yi)[16
     }
 }
 
-template <typename R, bool CPLX> using EncTile = R[CPLX ? 32 : 64][64 + 1][CPLX ? 2 : 1];
+// 64 k x 64 vectors (real) or 32 k x 64 vectors x re/im (complex), rows padded by one element.  OZ2_ENC_SWZ=1 (A/B
+// builds): the real tile unpadded with the vector index XORed by the k index (32 KiB: five blocks per CU instead
+// of four); same bits and the same time (cfg2 split 0.694 / 0.695 ms, profiles/r06/enc_swizzle_ab.txt)
+#ifndef OZ2_ENC_SWZ
+#define OZ2_ENC_SWZ 0
+#endif
+template <typename R, bool CPLX>
+using EncTile = R[CPLX ? 32 : 64][CPLX || !OZ2_ENC_SWZ ? 65 : 64][CPLX ? 2 : 1];
+template <bool CPLX> __device__ __forceinline__ int etx(int el, int vl) { return CPLX || !OZ2_ENC_SWZ ? vl : vl ^ el; }
 
 // Accurate mode, real operands, one stream: the final shifts computed by the encode itself from sft0 and the bound
 // maxima (finalize_accurate_sft_kernel's arithmetic), stored by the blocks of the first k-tile
@@ -790,8 +798,8 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
         const int idx = tid + NT * i;
         int vl, el;
         if (CONTIG) { el = idx % KT; vl = idx / KT; } else { vl = idx & 63; el = idx >> 6; }
-        tile[el][vl][0] = lre[i];
-        if (CPLX) tile[el][vl][NC - 1] = (flags & ENC_CONJ) ? -lim[i] : lim[i];
+        tile[el][etx<CPLX>(el, vl)][0] = lre[i];
+        if (CPLX) tile[el][etx<CPLX>(el, vl)][NC - 1] = (flags & ENC_CONJ) ? -lim[i] : lim[i];
     }
     __syncthreads();
 
@@ -804,8 +812,8 @@ __device__ __forceinline__ void encode_body(const R *__restrict__ X, size_t ld, 
     R yr[16], yi[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        R re = tile[16 * c + q][vl][0];
-        R im = CPLX ? tile[16 * c + q][vl][NC - 1] : R(0);
+        R re = tile[16 * c + q][etx<CPLX>(16 * c + q, vl)][0];
+        R im = CPLX ? tile[16 * c + q][etx<CPLX>(16 * c + q, vl)][NC - 1] : R(0);
         if (MODE != 1) {
             yr[q] = trunc(scalbn(re, s));
             yi[q] = trunc(scalbn(im, s));
@@ -884,7 +892,7 @@ __device__ __forceinline__ void mag_tile_body(const R *__restrict__ X, size_t ld
     for (int i = 0; i < NL; ++i) {
         const int idx = tid + 256 * i;
         const int el = CONTIG ? idx % 64 : idx >> 6, vl = CONTIG ? idx / 64 : idx & 63;
-        tile[el][vl][0] = lre[i];
+        tile[el][etx<false>(el, vl)][0] = lre[i];
     }
     __syncthreads();
     // the 4 lanes of a vector's tile row are neighbours in one wave (c-th 16-element chunk): its tile
@@ -894,7 +902,7 @@ __device__ __forceinline__ void mag_tile_body(const R *__restrict__ X, size_t ld
     int nan = 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-        x[q] = fabs(tile[16 * c + q][vl][0]);
+        x[q] = fabs(tile[16 * c + q][etx<false>(16 * c + q, vl)][0]);
         mx = fmax(mx, x[q]);  // NaN ignored, as the stats pass's amax
         if (x[q] != R(0) && x[q] < mn) mn = x[q];
         nan |= __builtin_isnan(x[q]) ? 1 : 0;
