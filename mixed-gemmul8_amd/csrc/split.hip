@@ -1139,12 +1139,13 @@ __global__ __launch_bounds__(CPLX ? 128 : 256) void encode_pair_kernel(EncOperan
 
 // ------------------------------------------------------------------
 // Fast mode, small k, one stream: shifts and slices of both operands in ONE launch that reads each operand once.
-// A block holds FZ_V = 4 (GEMMUL8_FUSED_V=8: 8) whole vectors (k <= KMAX elements each, f64) in LDS: it loads them (coalesced along
-// whichever index is contiguous), sums them in the reference's order -- wave w takes vector w, lane l the
-// reference's virtual threads l and l + 64 of VT = 128 (their round-up chains in element order), then the
-// tail of stats_strided_body -- and encodes its vectors from the same LDS copy (encode_vec16, MODE 0).  Same
+// A block holds FZ_V = 4 (GEMMUL8_FUSED_V=8: 8) whole vectors (k <= KMAX elements each, f64) in LDS: it loads them
+// (coalesced along whichever index is contiguous), sums them in the reference's order -- wave w takes vector w,
+// lane l the reference's virtual threads l and l + 64 of VT = 128 (their round-up chains in element order), then
+// the tail of stats_strided_body -- and encodes its vectors from the same LDS copy (encode_vec16, MODE 0).  Same
 // shifts and bytes as split_stats_pair + split_encode_pair (tests/test_gpu_parity.py), one launch and one
-// operand read instead of two each.  Blocks [0, na) take A's vectors, the rest B's.
+// operand read instead of two each.  Blocks [0, na) take A's vectors, the rest B's.  MAG: accurate mode's first
+// pass in the same form (sft0 from the vector amax, the 6-bit magnitudes, MODE 1).
 // ------------------------------------------------------------------
 // A/B builds (profiles/r06/fused_split/): OZ2_FZ_PAD=1 pads 16 bytes after every 16 elements of the LDS panel
 // (the encode's chunks 144 bytes apart), OZ2_FZ_XCD_CONTIG=1 renumbers a contiguous operand's blocks onto one
