@@ -1541,7 +1541,13 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         }
         return;
     }
-    if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || ntiles_all >= 3 * ncu)) {
+    // round 6, per-group kernel: also up to 1.5 tiles per CU from 16 k-steps per tile (no second launch round:
+    // 1024^3 products 22.7 -> 21.0 us, 1152^3 37.3 -> 36.3, 1280^3 44.6 -> 39.2; below 16 k-steps it loses: 512^3
+    // 12.8 -> 19.2, 768^3 15.8 -> 22.2; 1536^3, 2 per CU, stays one-tile: 54.4 vs 60.2;
+    // profiles/r06/mid_sizes/persistent_ab.txt)
+    const bool persist_rule =
+        ntiles_all >= 3 * ncu || (pg_epilogue() && 2 * ntiles_all <= 3 * ncu && g.ksteps >= 16);
+    if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || persist_rule)) {
         g_last_residue_kernel.store(2, std::memory_order_relaxed);
         g.nplanes = nplanes * g.nsub;
         g.queue = queue;

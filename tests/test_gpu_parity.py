@@ -833,13 +833,16 @@ def test_small_tiles_match_one_tile():
                 assert np.array_equal(outs["onetile"][key].view(np.uint8), outs[name][key].view(np.uint8)), (name, key)
         assert str(outs["forced"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
         assert str(outs["forced"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_small_kernel"
-        assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
+        # (1024^3: 224 tiles on 256 CUs, at most 1.5 per CU: the persistent per-group kernel since round 6)
+        assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_persistent_pg_kernel"
         assert str(outs["default"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_persistent_pg_kernel"
         # tail planes: 2048^3 (3.5 tiles per CU) 12 planes on the persistent kernel (3 rounds), the last 2 as
-        # 128 x 128 tiles; 1152^3 (350 tiles on 256 CUs) 10 planes on the one-tile kernel and 4 as 128 x 128 tiles
+        # 128 x 128 tiles; 1152^3 (350 tiles on 256 CUs) 10 planes on the persistent kernel (250 tiles, one round)
+        # and 4 as 128 x 128 tiles
         assert str(outs["tail"]["2048_2048_2048_14_True_d_kernel"][0]) == \
             "gemm_i8_persistent_pg_kernel+gemm_i8_small_kernel"
-        assert str(outs["tail"]["1152_1152_1152_14_True_d_kernel"][0]) == "gemm_i8_kernel+gemm_i8_small_kernel"
+        assert str(outs["tail"]["1152_1152_1152_14_True_d_kernel"][0]) == \
+            "gemm_i8_persistent_pg_kernel+gemm_i8_small_kernel"
         assert str(outs["onetile"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
     code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
             "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
