@@ -1101,6 +1101,9 @@ __device__ __forceinline__ void mfma_step_first(AccTile (&acc)[ACC_I][ACC_J], co
 
 // ABL (probe builds, tools/probes/persist_pg_ab.hip): 1 = residues reduced to the low byte (wrong residues), 2 = no
 // residue stores, 3 = neither park nor stores (the epilogue's barriers only)
+#ifndef OZ2_PG_CLAIM_EARLY
+#define OZ2_PG_CLAIM_EARLY 1
+#endif
 template <bool SUB, int PRIO = 1, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(GemmArgs g) {
     static_assert(OZ2_MFMA16, "per-group epilogue: 16x16x64 accumulator map");
@@ -1127,7 +1130,11 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
     auto to_tile = [&](unsigned pos) { return pos + nblk < total ? pos + nblk : NO_TILE; };
     unsigned ccur = (bid >> 3) < total ? (bid >> 3) : NO_TILE;
     if (ccur == NO_TILE) return;  // block-uniform, before any barrier
-    if (tid == 0) spare[0] = to_tile(claim());
+    // the claim of the second tile is issued after the prologue DMA, so its round trip (a contended queue head)
+    // overlaps the first panels' latency; claimed first, the wait for its result (the compiler waits for every
+    // memory operation before the DMA's inline asm) held wave 0's DMA and with it every block's first k-step
+    // (OZ2_PG_CLAIM_EARLY=0: the old order, A/B builds)
+    if (!OZ2_PG_CLAIM_EARLY && tid == 0) spare[0] = to_tile(claim());
 
     const unsigned K = g.ksteps;  // >= 6 (host)
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
@@ -1148,6 +1155,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
         bglds16(rB, ct.offB + s0 * PANEL + lane_off, lo + PANEL);
         bglds16(rB, ct.offB + s0 * PANEL + lane_off + 8192, lo + PANEL + 8192);
     }
+    if (OZ2_PG_CLAIM_EARLY && tid == 0) spare[0] = to_tile(claim());
     wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();  // step 0 landed (and the claim's LDS write)
     barrier();
 
@@ -1197,7 +1205,11 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
         };
         step(wait01, std::true_type{}, [&] {
             if (claimed) {  // group 0's MFMA interval: group 1 has read its parked residues back
-                spare[0] = to_tile(pos);
+                // (the opaque copy keeps the compiler from using the claim's result -- and waiting for it, with
+                // every older memory operation -- right after the atomic in the epilogue)
+                unsigned p2 = pos;
+                if (OZ2_PG_CLAIM_EARLY) asm volatile("" : "+v"(p2));
+                spare[0] = to_tile(p2);
                 __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
             }
         });
