@@ -1553,12 +1553,18 @@ void gemm_i8(const int8_t *A8, const int8_t *B8, const Layout &L, unsigned nplan
         }
         return;
     }
-    // round 6, per-group kernel: also up to 1.5 tiles per CU from 16 k-steps per tile (no second launch round:
-    // 1024^3 products 22.7 -> 21.0 us, 1152^3 37.3 -> 36.3, 1280^3 44.6 -> 39.2; below 16 k-steps it loses: 512^3
-    // 12.8 -> 19.2, 768^3 15.8 -> 22.2; 1536^3, 2 per CU, stays one-tile: 54.4 vs 60.2;
-    // profiles/r06/mid_sizes/persistent_ab.txt)
-    const bool persist_rule =
-        ntiles_all >= 3 * ncu || (pg_epilogue() && 2 * ntiles_all <= 3 * ncu && g.ksteps >= 16);
+    // round 6, per-group kernel: also up to 1.5 tiles per CU when its XCD queues need no more rounds than the
+    // one-tile launch (1024^3 products 22.7 -> 21.0 us, 1152^3 37.3 -> 36.3, 1280^3 44.6 -> 39.2; 1024^2 x k
+    // faster from 6 k-steps on).  With fewer than 8 tiles per plane, or 9 of them, the XCD shares are uneven
+    // (512^2: 4 tiles per plane on 4 XCDs, 7 blocks each for 14 tiles, 2 rounds: 13.2 -> 19.5 us; 768^3 15.8 ->
+    // 22.2), so those stay one-tile; 1536^3 (2 per CU) too: 54.4 vs 60.2 (profiles/r06/mid_sizes/persistent_ab.txt)
+    auto persist_balanced = [&] {
+        const unsigned per_plane = (unsigned)(L.mtiles * L.ntiles), grid = std::min(ntiles_all, ncu);
+        const unsigned most = nplanes * g.nsub * ((per_plane >> 3) + ((per_plane & 7) ? 1u : 0u));
+        const unsigned fewest_blocks = grid >> 3;
+        return fewest_blocks > 0 && (most + fewest_blocks - 1) / fewest_blocks <= (ntiles_all + ncu - 1) / ncu;
+    };
+    const bool persist_rule = ntiles_all >= 3 * ncu || (pg_epilogue() && 2 * ntiles_all <= 3 * ncu && persist_balanced());
     if (epi == Epi::RESIDUE && queue && buf && pmode != 0 && g.ksteps >= 6 && (pmode == 1 || persist_rule)) {
         g_last_residue_kernel.store(2, std::memory_order_relaxed);
         g.nplanes = nplanes * g.nsub;

@@ -837,12 +837,11 @@ def test_small_tiles_match_one_tile():
         assert str(outs["default"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_persistent_pg_kernel"
         assert str(outs["default"]["2048_2048_2048_14_True_d_kernel"][0]) == "gemm_i8_persistent_pg_kernel"
         # tail planes: 2048^3 (3.5 tiles per CU) 12 planes on the persistent kernel (3 rounds), the last 2 as
-        # 128 x 128 tiles; 1152^3 (350 tiles on 256 CUs) 10 planes on the persistent kernel (250 tiles, one round)
-        # and 4 as 128 x 128 tiles
+        # 128 x 128 tiles; 1152^3 (350 tiles on 256 CUs) 10 planes on the one-tile kernel (250 tiles: uneven XCD
+        # shares of 25 tiles per plane would take the persistent kernel two rounds) and 4 as 128 x 128 tiles
         assert str(outs["tail"]["2048_2048_2048_14_True_d_kernel"][0]) == \
             "gemm_i8_persistent_pg_kernel+gemm_i8_small_kernel"
-        assert str(outs["tail"]["1152_1152_1152_14_True_d_kernel"][0]) == \
-            "gemm_i8_persistent_pg_kernel+gemm_i8_small_kernel"
+        assert str(outs["tail"]["1152_1152_1152_14_True_d_kernel"][0]) == "gemm_i8_kernel+gemm_i8_small_kernel"
         assert str(outs["onetile"]["1024_1024_1024_14_True_d_kernel"][0]) == "gemm_i8_kernel"
     code = ("import sys, numpy as np; sys.path[:0] = sys.argv[1:4]\n"
             "from test_gpu_parity import check_full\nfrom util import randmat_np\n"
