@@ -1102,7 +1102,7 @@ __device__ __forceinline__ void mfma_step_first(AccTile (&acc)[ACC_I][ACC_J], co
 // ABL (probe builds, tools/probes/persist_pg_ab.hip): 1 = residues reduced to the low byte (wrong residues), 2 = no
 // residue stores, 3 = neither park nor stores (the epilogue's barriers only)
 #ifndef OZ2_PG_CLAIM_EARLY
-#define OZ2_PG_CLAIM_EARLY 1
+#define OZ2_PG_CLAIM_EARLY 0
 #endif
 template <bool SUB, int PRIO = 1, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(GemmArgs g) {
@@ -1130,10 +1130,10 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
     auto to_tile = [&](unsigned pos) { return pos + nblk < total ? pos + nblk : NO_TILE; };
     unsigned ccur = (bid >> 3) < total ? (bid >> 3) : NO_TILE;
     if (ccur == NO_TILE) return;  // block-uniform, before any barrier
-    // the claim of the second tile is issued after the prologue DMA, so its round trip (a contended queue head)
-    // overlaps the first panels' latency; claimed first, the wait for its result (the compiler waits for every
-    // memory operation before the DMA's inline asm) held wave 0's DMA and with it every block's first k-step
-    // (OZ2_PG_CLAIM_EARLY=0: the old order, A/B builds)
+    // the claim of the second tile, before the prologue DMA (waited for at once).  OZ2_PG_CLAIM_EARLY=1 (A/B builds)
+    // issues it after the DMA, overlapping the two latencies: same time, but the blocks' second tiles then come
+    // out of dispatch order and the launch fetches 5 % more (11.9 vs 11.3 GB at cfg2,
+    // profiles/r06/epilogue_ab/claim_ab.txt)
     if (!OZ2_PG_CLAIM_EARLY && tid == 0) spare[0] = to_tile(claim());
 
     const unsigned K = g.ksteps;  // >= 6 (host)
@@ -1208,7 +1208,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
                 // (the opaque copy keeps the compiler from using the claim's result -- and waiting for it, with
                 // every older memory operation -- right after the atomic in the epilogue)
                 unsigned p2 = pos;
-                if (OZ2_PG_CLAIM_EARLY) asm volatile("" : "+v"(p2));
+                asm volatile("" : "+v"(p2));
                 spare[0] = to_tile(p2);
                 __builtin_amdgcn_s_waitcnt((15) | (7 << 4) | (0 << 8) | (3 << 14));  // lgkmcnt(0)
             }
