@@ -1104,6 +1104,9 @@ __device__ __forceinline__ void mfma_step_first(AccTile (&acc)[ACC_I][ACC_J], co
 #ifndef OZ2_PG_CLAIM_EARLY
 #define OZ2_PG_CLAIM_EARLY 0
 #endif
+#ifndef OZ2_PG_STATIC2
+#define OZ2_PG_STATIC2 1
+#endif
 template <bool SUB, int PRIO = 1, int ABL = 0>
 __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(GemmArgs g) {
     static_assert(OZ2_MFMA16, "per-group epilogue: 16x16x64 accumulator map");
@@ -1127,14 +1130,20 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
         return y * P + basex + (i - y * tx);
     };
     auto claim = [&]() { return __hip_atomic_fetch_add(g.queue + xcd, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto to_tile = [&](unsigned pos) { return pos + nblk < total ? pos + nblk : NO_TILE; };
+    // queue positions count from the block's third tile when the second is static (OZ2_PG_STATIC2)
+    constexpr unsigned STATIC_TILES = OZ2_PG_STATIC2 ? 2 : 1;
+    auto to_tile = [&](unsigned pos) { return pos + STATIC_TILES * nblk < total ? pos + STATIC_TILES * nblk : NO_TILE; };
     unsigned ccur = (bid >> 3) < total ? (bid >> 3) : NO_TILE;
     if (ccur == NO_TILE) return;  // block-uniform, before any barrier
-    // the claim of the second tile, before the prologue DMA (waited for at once).  OZ2_PG_CLAIM_EARLY=1 (A/B builds)
-    // issues it after the DMA, overlapping the two latencies: same time, but the blocks' second tiles then come
-    // out of dispatch order and the launch fetches 5 % more (11.9 vs 11.3 GB at cfg2,
-    // profiles/r06/epilogue_ab/claim_ab.txt)
-    if (!OZ2_PG_CLAIM_EARLY && tid == 0) spare[0] = to_tile(claim());
+    // the second tile: static, the block's position plus the XCD's block count (OZ2_PG_STATIC2, the default: no
+    // atomic round trip before the first DMA), or claimed before the prologue DMA and waited for at once.
+    // OZ2_PG_CLAIM_EARLY=1 (A/B builds) issued that claim after the DMA: same time, but the blocks' second tiles
+    // then left dispatch order and the launch fetched 5 % more (profiles/r06/epilogue_ab/claim_ab.txt)
+    if (OZ2_PG_STATIC2 && tid == 0) {
+        const unsigned second = nblk + (bid >> 3);
+        spare[0] = second < total ? second : NO_TILE;
+    }
+    if (!OZ2_PG_STATIC2 && !OZ2_PG_CLAIM_EARLY && tid == 0) spare[0] = to_tile(claim());
 
     const unsigned K = g.ksteps;  // >= 6 (host)
     const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int8_t *)smem;
@@ -1155,7 +1164,7 @@ __global__ __launch_bounds__(NTHREADS, 1) void gemm_i8_persistent_pg_kernel(Gemm
         bglds16(rB, ct.offB + s0 * PANEL + lane_off, lo + PANEL);
         bglds16(rB, ct.offB + s0 * PANEL + lane_off + 8192, lo + PANEL + 8192);
     }
-    if (OZ2_PG_CLAIM_EARLY && tid == 0) spare[0] = to_tile(claim());
+    if (!OZ2_PG_STATIC2 && OZ2_PG_CLAIM_EARLY && tid == 0) spare[0] = to_tile(claim());
     wait_vm_lgkm0<GLDS_PER_STEP *(D - 1)>();  // step 0 landed (and the claim's LDS write)
     barrier();
 
